@@ -1,0 +1,762 @@
+/*
+ * grm_device.h -- device-side physics of the transport hot path (HIP, gfx950).
+ *
+ * Same algorithm as the reference CPU path (m-torhan/cuda-grmonty, CPU semantics
+ * chosen over its CUDA port where they differ -- SURVEY.md §8 quirks Q1-Q8),
+ * written for CDNA4: all state in VGPRs, no 4x4 heap temporaries, shared trig
+ * between the metric and the connection at one point, iterative (stackless)
+ * geodesic sub-stepping, fp64 throughout.
+ *
+ * Included only by the .hip translation units of this package.
+ */
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/grmonty_amd.h"
+
+namespace grm {
+
+/* ---- constants: reference consts.hpp:14-157 (same literals) ---- */
+constexpr double kPi = 3.141592653589793238462643383279502884;
+constexpr double kSqrt2 = 1.414213562373095048801688724209698079;
+constexpr double EPS = 1.0e-40;
+constexpr double THETA_E_MIN = 0.3, TP_OVER_TE = 3.0;
+constexpr double WEIGHT_MIN = 1.0e31, ROULETTE = 1.0e4;
+constexpr double STEP_EPS = 0.04, E_TOL = 1.0e-3;
+constexpr int MAX_ITER = 2, MAX_N_STEP = 1280000, MAX_SUBDIV = 7;
+constexpr double EE = 4.80320680e-10, CL = 2.99792458e10, ME = 9.1093826e-28, MP = 1.67262171e-24;
+constexpr double HPL = 6.6260693e-27;
+constexpr double SIGMA_THOMSON = 0.665245873e-24;
+constexpr double HC_MIN_W = 1.0e-12, HC_MAX_W = 1.0e6, HC_MIN_T = 1.0e-4, HC_MAX_T = 1.0e4;
+constexpr int HC_N_T = 80;
+constexpr double HC_MAX_GAMMA = 12.0, HC_D_MU_E = 0.05, HC_D_GAMMA_E = 0.05;
+constexpr double JNU_MAX_T = 1.0e2, JNU_CST = 1.88774862536;
+constexpr double SPEC_D_L_E = 0.25;
+constexpr int N_TH_BINS = GRM_N_TH_BINS, N_E_BINS = GRM_N_E_BINS;
+
+/* Kernel-argument block: everything uniform across lanes (lands in SGPRs). */
+struct Params {
+    int n1, n2;
+    double xs1, xs2, xe1, xe2, dx1, dx2; /* x_start/x_stop/dx of dims 1,2 */
+    double a, h_slope, r0;
+    double n_e_unit, theta_e_unit, b_unit;
+    double x1_min, x1_max, d_tau_k, bias_norm;
+    double hc_l_min_w, hc_l_min_t, hc_d_l_w, hc_d_l_t;
+    double jnu_l_min_t, jnu_d_l_t;
+    double spec_l_e_0, th_dx2;
+    const double *zones;    /* [n1*n2][8]: rho,u,u1,u2,u3,B1,B2,B3 (64 B per zone) */
+    const double *hotcross; /* [221][81] log10 sigma */
+    const double *k2;       /* [201] log K2 */
+};
+
+/* ------------------------------------------------------------------------- */
+/* Philox4x32-10 per-photon streams (counter = (draw index, photon id))       */
+/* ------------------------------------------------------------------------- */
+struct Rng {
+    uint32_t k0, k1;
+    uint64_t id, ctr;
+};
+
+__device__ __forceinline__ void philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                             uint32_t k1, uint32_t &o0, uint32_t &o1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0;
+        const uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    o0 = c0;
+    o1 = c1;
+}
+
+/* uniform double in (0, 1] from 53 random bits */
+__device__ __forceinline__ double uniform(Rng &g) {
+    uint32_t o0, o1;
+    philox_block((uint32_t)g.ctr, (uint32_t)(g.ctr >> 32), (uint32_t)g.id, (uint32_t)(g.id >> 32), g.k0, g.k1, o0,
+                 o1);
+    ++g.ctr;
+    const uint64_t m = ((((uint64_t)o1) << 32) | o0) >> 11;
+    return (double)(m + 1) * (1.0 / 9007199254740992.0);
+}
+
+/* chi^2(dof) for dof 3..6: -2 ln(prod of dof/2 uniforms) (+ one Box-Muller normal^2 if odd) */
+__device__ __forceinline__ double chi_sq(Rng &g, int dof) {
+    double prod = uniform(g);
+    const int m = dof >> 1;
+    for (int i = 1; i < m; ++i) prod *= uniform(g);
+    double x = -2.0 * log(prod);
+    if (dof & 1) {
+        const double ua = uniform(g);
+        const double ub = uniform(g);
+        const double z = sqrt(-2.0 * log(ua)) * cos(2.0 * kPi * ub);
+        x += z * z;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t child_id(uint64_t parent_id, uint64_t parent_ctr) {
+    return splitmix64(parent_id ^ (0x9E3779B97F4A7C15ull * (parent_ctr + 1)));
+}
+
+/* ------------------------------------------------------------------------- */
+/* metric (harm_model.cpp:473-530, 1632-1637): one set of transcendentals per  */
+/* point, shared by g_cov, the row g^{0mu} and the connection.                */
+/* ------------------------------------------------------------------------- */
+struct Trig {
+    double r1;       /* exp(x1) */
+    double s2x, c2x; /* sin/cos(2 pi x2) */
+    double sth, cth; /* sin/cos(theta_BL) */
+};
+
+__device__ __forceinline__ void trig_at(const Params &P, const double x[4], Trig &T) {
+    T.r1 = exp(x[1]);
+    sincos(2.0 * kPi * x[2], &T.s2x, &T.c2x);
+    const double th = kPi * x[2] + ((1.0 - P.h_slope) / 2.0) * T.s2x;
+    sincos(th, &T.sth, &T.cth);
+}
+
+/* non-zero g_mu,nu of MKS Kerr + g^{00}, g^{01} (g^{02} = g^{03} = 0) */
+struct Gcov {
+    double g00, g01, g03, g11, g13, g22, g33;
+    double gn00, gn01;
+};
+
+__device__ __forceinline__ void gcov_from_trig(const Params &P, const Trig &T, Gcov &G) {
+    const double r = T.r1 + P.r0;
+    const double a = P.a;
+    const double sin_theta = fabs(T.sth) + EPS;
+    const double cos_theta = T.cth;
+    const double s2 = sin_theta * sin_theta;
+    const double rho2 = r * r + a * a * cos_theta * cos_theta;
+    const double rfac = r - P.r0;
+    const double hfac = kPi + (1.0 - P.h_slope) * kPi * T.c2x;
+    const double two_r_rho2 = 2.0 * r / rho2;
+    G.g00 = (-1.0 + two_r_rho2);
+    G.g01 = two_r_rho2 * rfac;
+    G.g03 = (-2.0 * a * r * s2 / rho2);
+    G.g11 = (1.0 + two_r_rho2) * rfac * rfac;
+    G.g13 = (-a * s2 * (1.0 + two_r_rho2)) * rfac;
+    G.g22 = rho2 * hfac * hfac;
+    G.g33 = s2 * (rho2 + a * a * s2 * (1.0 + two_r_rho2));
+    const double irho2 = 1.0 / rho2;
+    G.gn00 = -1.0 - 2.0 * r * irho2;
+    G.gn01 = 2.0 * irho2;
+}
+
+__device__ __forceinline__ void lower(const Gcov &G, const double u[4], double uc[4]) {
+    uc[0] = G.g00 * u[0] + G.g01 * u[1] + G.g03 * u[3];
+    uc[1] = G.g01 * u[0] + G.g11 * u[1] + G.g13 * u[3];
+    uc[2] = G.g22 * u[2];
+    uc[3] = G.g03 * u[0] + G.g13 * u[1] + G.g33 * u[3];
+}
+
+__device__ __forceinline__ void gcov_full(const Gcov &G, double g[4][4]) {
+    g[0][0] = G.g00; g[0][1] = G.g01; g[0][2] = 0.0; g[0][3] = G.g03;
+    g[1][0] = G.g01; g[1][1] = G.g11; g[1][2] = 0.0; g[1][3] = G.g13;
+    g[2][0] = 0.0;   g[2][1] = 0.0;   g[2][2] = G.g22; g[2][3] = 0.0;
+    g[3][0] = G.g03; g[3][1] = G.g13; g[3][2] = 0.0; g[3][3] = G.g33;
+}
+
+/* ------------------------------------------------------------------------- */
+/* connection (harm_model.cpp:1436-1569): 40 symmetric entries, j<=k;          */
+/* entries identically zero (1,0,2) (1,2,3) (2,0,2) (2,2,3) are dropped.       */
+/* ------------------------------------------------------------------------- */
+struct Conn {
+    double c[4][10]; /* [i][tri(j,k)], tri: 00 01 02 03 11 12 13 22 23 33 */
+};
+
+__device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn &C) {
+    const double r1 = T.r1, r2 = r1 * r1, r3 = r2 * r1, r4 = r3 * r1;
+    const double hs = P.h_slope;
+    const double dthdx2 = kPi * (1.0 + (1.0 - hs) * T.c2x);
+    const double d2thdx22 = -2.0 * kPi * kPi * (1.0 - hs) * T.s2x;
+    const double dthdx22 = dthdx2 * dthdx2;
+    const double sth = T.sth, cth = T.cth;
+    const double sth2 = sth * sth, r1sth2 = r1 * sth2, sth4 = sth2 * sth2;
+    const double cth2 = cth * cth, cth4 = cth2 * cth2;
+    const double s2th = 2.0 * sth * cth, c2th = 2.0 * cth2 - 1.0;
+    const double a = P.a, a2 = a * a, a3 = a2 * a, a4 = a3 * a;
+    const double a2sth2 = a2 * sth2, a2cth2 = a2 * cth2, a4cth4 = a4 * cth4;
+    const double rho2 = r2 + a2cth2, rho22 = rho2 * rho2, rho23 = rho22 * rho2;
+    const double irho2 = 1.0 / rho2, irho22 = irho2 * irho2, irho23 = irho22 * irho2;
+    const double irho23_dthdx2 = irho23 / dthdx2;
+    const double fac1 = r2 - a2cth2, fac1_rho23 = fac1 * irho23;
+    const double fac2 = a2 + 2.0 * r2 + a2 * c2th;
+    const double fac3 = a2 + r1 * (-2.0 + r1);
+    const double i_r1rho23 = 1.0 / (r1 * rho23);
+    const double i_sth = 1.0 / sth;
+
+    C.c[0][0] = 2.0 * r1 * fac1_rho23;
+    C.c[0][1] = r1 * (2.0 * r1 + rho2) * fac1_rho23;
+    C.c[0][2] = -a2 * r1 * s2th * dthdx2 * irho22;
+    C.c[0][3] = -2.0 * a * r1sth2 * fac1_rho23;
+    C.c[0][4] = 2.0 * r2 * (r4 + r1 * fac1 - a4cth4) * irho23;
+    C.c[0][5] = -a2 * r2 * s2th * dthdx2 * irho22;
+    C.c[0][6] = a * r1 * (-r1 * (r3 + 2.0 * fac1) + a4cth4) * sth2 * irho23;
+    C.c[0][7] = -2.0 * r2 * dthdx22 * irho2;
+    C.c[0][8] = a3 * r1sth2 * s2th * dthdx2 * irho22;
+    C.c[0][9] = 2.0 * r1sth2 * (-r1 * rho22 + a2sth2 * fac1) * irho23;
+
+    C.c[1][0] = fac3 * fac1 * i_r1rho23;
+    C.c[1][1] = fac1 * (-2.0 * r1 + a2sth2) * irho23;
+    C.c[1][2] = 0.0;
+    C.c[1][3] = -a * sth2 * fac3 * fac1 * i_r1rho23;
+    C.c[1][4] = (r4 * (-2.0 + r1) * (1.0 + r1) +
+                 a2 * (a2 * r1 * (1.0 + 3.0 * r1) * cth4 + a4cth4 * cth2 + r3 * sth2 +
+                       r1 * cth2 * (2.0 * r1 + 3.0 * r3 - a2sth2))) *
+                irho23;
+    C.c[1][5] = -a2 * dthdx2 * s2th / fac2;
+    C.c[1][6] = a * sth2 * (a4 * r1 * cth4 + r2 * (2.0 * r1 + r3 - a2sth2) + a2cth2 * (2.0 * r1 * (-1.0 + r2) + a2sth2)) *
+                irho23;
+    C.c[1][7] = -fac3 * dthdx22 * irho2;
+    C.c[1][8] = 0.0;
+    C.c[1][9] = -fac3 * sth2 * (r1 * rho22 - a2 * fac1 * sth2) * i_r1rho23;
+
+    C.c[2][0] = -a2 * r1 * s2th * irho23_dthdx2;
+    C.c[2][1] = r1 * C.c[2][0];
+    C.c[2][2] = 0.0;
+    C.c[2][3] = a * r1 * (a2 + r2) * s2th * irho23_dthdx2;
+    C.c[2][4] = r2 * C.c[2][0];
+    C.c[2][5] = r2 * irho2;
+    C.c[2][6] = (a * r1 * cth * sth * (r3 * (2.0 + r1) + a2 * (2.0 * r1 * (1.0 + r1) * cth2 + a2 * cth4 + 2.0 * r1sth2))) *
+                irho23_dthdx2;
+    C.c[2][7] = -a2 * cth * sth * dthdx2 * irho2 + d2thdx22 / dthdx2;
+    C.c[2][8] = 0.0;
+    C.c[2][9] = -cth * sth * (rho23 + a2sth2 * rho2 * (r1 * (4.0 + r1) + a2cth2) + 2.0 * r1 * a4 * sth4) *
+                irho23_dthdx2;
+
+    C.c[3][0] = a * fac1_rho23;
+    C.c[3][1] = r1 * C.c[3][0];
+    C.c[3][2] = -2.0 * a * r1 * cth * dthdx2 * i_sth / rho22;
+    C.c[3][3] = -a2sth2 * fac1_rho23;
+    C.c[3][4] = a * r2 * fac1_rho23;
+    C.c[3][5] = -2 * a * r1 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * cth * dthdx2 * i_sth / (fac2 * fac2);
+    C.c[3][6] = r1 * (r1 * rho22 - a2sth2 * fac1) * irho23;
+    C.c[3][7] = -a * r1 * dthdx22 * irho2;
+    C.c[3][8] = dthdx2 * (0.25 * fac2 * fac2 * cth * i_sth + a2 * r1 * s2th) * irho22;
+    C.c[3][9] = (-a * r1sth2 * rho22 + a3 * sth4 * fac1) * irho23;
+}
+
+/* dk^i/dlambda = -Gamma^i_{jk} k^j k^k (harm_model.cpp:1255-1262, 1578-1586) */
+__device__ __forceinline__ double geo_rhs(const Conn &C, int i, const double k[4]) {
+    const double *L = C.c[i];
+    double d = -2.0 * (k[0] * (L[1] * k[1] + L[2] * k[2] + L[3] * k[3]) + k[1] * (L[5] * k[2] + L[6] * k[3]) +
+                       L[8] * k[2] * k[3]);
+    d -= (L[0] * k[0] * k[0] + L[4] * k[1] * k[1] + L[7] * k[2] * k[2] + L[9] * k[3] * k[3]);
+    return d;
+}
+
+__device__ __forceinline__ void init_dkdlam(const Params &P, const double x[4], const double k[4], double dk[4]) {
+    Trig T;
+    trig_at(P, x, T);
+    Conn C;
+    connection(P, T, C);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dk[i] = geo_rhs(C, i, k);
+}
+
+/* harm_model.cpp:1620-1630 */
+__device__ __forceinline__ double step_size(const Params &P, const double x[4], const double k[4]) {
+    const double dl_x_1 = STEP_EPS * x[1] / (fabs(k[1]) + EPS);
+    const double dl_x_2 = STEP_EPS * fmin(x[2], P.xe2 - x[2]) / (fabs(k[2]) + EPS);
+    const double dl_x_3 = STEP_EPS / (fabs(k[3]) + EPS);
+    const double i1 = 1.0 / (fabs(dl_x_1) + EPS);
+    const double i2 = 1.0 / (fabs(dl_x_2) + EPS);
+    const double i3 = 1.0 / (fabs(dl_x_3) + EPS);
+    return 1.0 / (i1 + i2 + i3);
+}
+
+/* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
+ * predicate of :1279 and the new energy e_1; leaves Gcov at the new x in G. */
+__device__ __forceinline__ bool push_attempt(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
+                                             double dl, double &e_1, Gcov &G) {
+    const double dl_2 = 0.5 * dl;
+    double kp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double d = dk[i] * dl_2;
+        k[i] += d;
+        kp[i] = k[i] + d;
+        x[i] += k[i] * dl;
+    }
+    Trig T;
+    trig_at(P, x, T);
+    Conn C;
+    connection(P, T, C);
+    double err;
+    int iter = 0;
+    do {
+        ++iter;
+        const double kc[4] = {kp[0], kp[1], kp[2], kp[3]};
+        err = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            dk[i] = geo_rhs(C, i, kc);
+            kp[i] = k[i] + dl_2 * dk[i];
+            err += fabs((kc[i] - kp[i]) / (kp[i] + EPS));
+        }
+    } while (err > E_TOL && iter < MAX_ITER);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k[i] = kp[i];
+    gcov_from_trig(P, T, G);
+    e_1 = -(k[0] * G.g00 + k[1] * G.g01 + k[3] * G.g03);
+    const double err_e = fabs((e_1 - e_0_s) / e_0_s);
+    return (err_e > 1.0e-4 || err > E_TOL || isnan(err) || isinf(err));
+}
+
+/* Per-lane spill slot for the push backup, laid out [component][lane] so that a wave's
+ * accesses are consecutive 8-B words (conflict-free ds_read_b64 / ds_write_b64).  The
+ * transport kernel points it at LDS; the probe kernel at a private array. */
+struct Slot {
+    double *p;
+    int stride;
+    __device__ __forceinline__ double &operator[](int i) const { return p[i * stride]; }
+};
+
+/* push_photon (harm_model.cpp:1217-1289) without recursion: a depth-first walk of the
+ * halving tree.  Bit k of `pend` marks a pending second half at depth k.  Sub-step length
+ * dl * 2^-depth is exact (power-of-two scaling), as the reference's 0.5*dl chain is.
+ * bk: 12-double backup of (x, k, dk) at the start of the current attempt. */
+__device__ __forceinline__ void push_photon(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
+                                            double dl, const Slot &bk) {
+    int depth = 0;
+    uint32_t pend = 0;
+    while (true) {
+        if (!(x[1] < P.xs1)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                bk[i] = x[i];
+                bk[4 + i] = k[i];
+                bk[8 + i] = dk[i];
+            }
+            double e_1;
+            Gcov G;
+            const bool fail = push_attempt(P, x, k, dk, e_0_s, ldexp(dl, -depth), e_1, G);
+            if (fail && depth < MAX_SUBDIV) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    x[i] = bk[i];
+                    k[i] = bk[4 + i];
+                    dk[i] = bk[8 + i];
+                }
+                ++depth;
+                pend |= 1u << depth;
+                continue;
+            }
+            e_0_s = e_1;
+        }
+        if (pend == 0) break;
+        depth = 31 - __builtin_clz(pend);
+        pend &= ~(1u << depth);
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* fluid (harm_model.cpp:595-671, x_to_ij 1406-1434, interp_scalar 1646-1656) */
+/* ------------------------------------------------------------------------- */
+struct Fluid {
+    double n_e, theta_e, b;
+    double u_con[4], u_cov[4], b_con[4], b_cov[4];
+};
+
+__device__ __forceinline__ void fluid_params(const Params &P, const double x[4], const Gcov &G, Fluid &F) {
+    if (x[1] < P.xs1 || x[1] > P.xe1 || x[2] < P.xs2 || x[2] > P.xe2) {
+        /* out of grid: n_e = 0; the reference leaves the rest unset, we zero it (so does the oracle) */
+        F.n_e = F.theta_e = F.b = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F.u_con[q] = F.u_cov[q] = F.b_con[q] = F.b_cov[q] = 0.0;
+        return;
+    }
+    int i = (int)((x[1] - P.xs1) / P.dx1 - 0.5 + 1000) - 1000;
+    int j = (int)((x[2] - P.xs2) / P.dx2 - 0.5 + 1000) - 1000;
+    double di, dj;
+    if (i < 0) {
+        i = 0;
+        di = 0.0;
+    } else if (i > P.n1 - 2) {
+        i = P.n1 - 2;
+        di = 1.0;
+    } else {
+        di = (x[1] - ((i + 0.5) * P.dx1 + P.xs1)) / P.dx1;
+    }
+    if (j < 0) {
+        j = 0;
+        dj = 0.0;
+    } else if (j > P.n2 - 2) {
+        j = P.n2 - 2;
+        dj = 1.0;
+    } else {
+        dj = (x[2] - ((j + 0.5) * P.dx2 + P.xs2)) / P.dx2;
+    }
+    const double c0 = (1.0 - di) * (1.0 - dj), c1 = (1.0 - di) * dj, c2 = di * (1.0 - dj), c3 = di * dj;
+    /* 4 zones x 64 B, each as 4 x 16-B loads */
+    const double2 *z00 = reinterpret_cast<const double2 *>(P.zones + ((size_t)i * P.n2 + j) * 8);
+    const double2 *z10 = reinterpret_cast<const double2 *>(P.zones + ((size_t)(i + 1) * P.n2 + j) * 8);
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double2 a = z00[q], b = z00[q + 4], c = z10[q], d = z10[q + 4];
+        v[2 * q] = a.x * c0 + b.x * c1 + c.x * c2 + d.x * c3;
+        v[2 * q + 1] = a.y * c0 + b.y * c1 + c.y * c2 + d.y * c3;
+    }
+    const double rho = v[0], uu = v[1];
+    F.n_e = rho * P.n_e_unit;
+    F.theta_e = uu / rho * P.theta_e_unit;
+    const double vc1 = v[2], vc2 = v[3], vc3 = v[4];
+    const double bp1 = v[5], bp2 = v[6], bp3 = v[7];
+    const double vdv = G.g11 * vc1 * vc1 + G.g13 * vc1 * vc3 + G.g22 * vc2 * vc2 + G.g13 * vc3 * vc1 + G.g33 * vc3 * vc3;
+    const double vfac = sqrt(-1.0 / G.gn00 * (1.0 + fabs(vdv)));
+    F.u_con[0] = -vfac * G.gn00;
+    F.u_con[1] = vc1 - vfac * G.gn01;
+    F.u_con[2] = vc2;
+    F.u_con[3] = vc3;
+    lower(G, F.u_con, F.u_cov);
+    const double udb = F.u_cov[1] * bp1 + F.u_cov[2] * bp2 + F.u_cov[3] * bp3;
+    const double iu0 = 1.0 / F.u_con[0];
+    F.b_con[0] = udb;
+    F.b_con[1] = (bp1 + F.u_con[1] * udb) * iu0;
+    F.b_con[2] = (bp2 + F.u_con[2] * udb) * iu0;
+    F.b_con[3] = (bp3 + F.u_con[3] * udb) * iu0;
+    lower(G, F.b_con, F.b_cov);
+    F.b = sqrt(F.b_con[0] * F.b_cov[0] + F.b_con[1] * F.b_cov[1] + F.b_con[2] * F.b_cov[2] + F.b_con[3] * F.b_cov[3]) *
+          P.b_unit;
+}
+
+/* ------------------------------------------------------------------------- */
+/* radiation (radiation.cpp:59-146), hotcross lookup (hotcross.cpp:81-106),   */
+/* synchrotron (jnu_mixed.cpp:75-111, 150-158)                                */
+/* ------------------------------------------------------------------------- */
+__device__ __forceinline__ double bk_angle(const double k[4], const Fluid &F, double b_unit) {
+    if (F.b == 0.0) return kPi / 2.0;
+    const double k_ = fabs(k[0] * F.u_cov[0] + k[1] * F.u_cov[1] + k[2] * F.u_cov[2] + k[3] * F.u_cov[3]);
+    double mu = (k[0] * F.b_cov[0] + k[1] * F.b_cov[1] + k[2] * F.b_cov[2] + k[3] * F.b_cov[3]) / (k_ * F.b / b_unit);
+    mu = fmin(fmax(mu, -1.0), 1.0);
+    return acos(mu);
+}
+
+__device__ __forceinline__ double fluid_nu(const double k[4], const Fluid &F) {
+    const double energy = -(k[0] * F.u_cov[0] + k[1] * F.u_cov[1] + k[2] * F.u_cov[2] + k[3] * F.u_cov[3]);
+    return energy * ME * CL * CL / HPL;
+}
+
+__device__ __forceinline__ double hc_klein_nishina(double w) { /* hotcross.cpp:144-151 */
+    if (w < 1.0e-3) return (1.0 - 2.0 * w);
+    return (3.0 / 4.0) * (2.0 / (w * w) + (1.0 / (2.0 * w) - (1.0 + w) / (w * w * w)) * log(1.0 + 2.0 * w) +
+                          (1.0 + w) / ((1.0 + 2.0 * w) * (1.0 + 2.0 * w)));
+}
+
+/* e^x K_2(x) = int_0^inf exp(-x (cosh t - 1)) cosh 2t dt, trapezoid rule (spectrally accurate
+ * for this analytic integrand); double-precision replacement for std::cyl_bessel_k (Q5). */
+__device__ __noinline__ double k2_scaled(double x) {
+    const double h = 1.0 / 32.0;
+    double sum = 0.5;
+    for (int n = 1; n < 20000; ++n) {
+        const double t = n * h;
+        const double term = exp(-x * (cosh(t) - 1.0)) * cosh(2.0 * t);
+        sum += term;
+        if (term < 1.0e-18 * sum) break;
+    }
+    return sum * h;
+}
+
+/* total_compton_cross_num (hotcross.cpp:108-142): rare fallback outside the table */
+__device__ __noinline__ double hotcross_num(double w, double theta_e) {
+    if (isnan(w)) return 0.0;
+    if (theta_e < HC_MIN_T && w < HC_MIN_W) return SIGMA_THOMSON;
+    if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
+    const double k2f = (theta_e > 1.0e-2) ? k2_scaled(1.0 / theta_e) : sqrt(kPi * theta_e / 2.0);
+    double cross = 0.0;
+    for (double mu_e = -1.0 + 0.5 * HC_D_MU_E; mu_e < 1.0; mu_e += HC_D_MU_E) {
+        for (double g = 1.0 + 0.5 * theta_e * HC_D_GAMMA_E; g < 1.0 + HC_MAX_GAMMA * theta_e;
+             g += theta_e * HC_D_GAMMA_E) {
+            const double f = 0.5 * ((g * sqrt(g * g - 1.) / (theta_e * k2f)) * exp(-(g - 1.) / theta_e));
+            const double v = sqrt(g * g - 1.0) / g;
+            const double bc = hc_klein_nishina(w * g * (1.0 - mu_e * v)) * (1.0 - mu_e * v);
+            cross += theta_e * HC_D_MU_E * HC_D_GAMMA_E * bc * f;
+        }
+    }
+    return cross * SIGMA_THOMSON;
+}
+
+__device__ __forceinline__ double hotcross_lkup(const Params &P, double w, double theta_e) {
+    if (w * theta_e < 1.0e-6) return SIGMA_THOMSON;
+    if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
+    if (w <= HC_MIN_W || w >= HC_MAX_W || theta_e <= HC_MIN_T || theta_e >= HC_MAX_T) return hotcross_num(w, theta_e);
+    const double fi = (log10(w) - P.hc_l_min_w) / P.hc_d_l_w;
+    const double fj = (log10(theta_e) - P.hc_l_min_t) / P.hc_d_l_t;
+    const int i = (int)fi, j = (int)fj;
+    const double d_i = fi - i, d_j = fj - j;
+    const double *t = P.hotcross + (size_t)i * (HC_N_T + 1) + j;
+    const double t00 = t[0], t01 = t[1], t10 = t[HC_N_T + 1], t11 = t[HC_N_T + 2];
+    const double lc =
+        (1.0 - d_i) * (1.0 - d_j) * t00 + d_i * (1.0 - d_j) * t10 + (1.0 - d_i) * d_j * t01 + d_i * d_j * t11;
+    return exp10(lc);
+}
+
+__device__ __forceinline__ double k2_eval(const Params &P, double theta_e) {
+    if (theta_e < THETA_E_MIN) return 0.0;
+    if (theta_e > JNU_MAX_T) return 2.0 * theta_e * theta_e;
+    double d_i = (log(theta_e) - P.jnu_l_min_t) / P.jnu_d_l_t;
+    const int i = min((int)d_i, GRM_N_E_SAMP - 1); /* theta_e == 100 exactly: stay in the table */
+    d_i -= i;
+    return exp((1.0 - d_i) * P.k2[i] + d_i * P.k2[i + 1]);
+}
+
+__device__ __forceinline__ double synch(const Params &P, double nu, double n_e, double theta_e, double b,
+                                        double theta) {
+    if (theta_e < THETA_E_MIN) return 0.0;
+    const double k2 = k2_eval(P, theta_e);
+    const double nu_c = EE * b / (2.0 * kPi * ME * CL);
+    const double nu_s = (2.0 / 9.0) * nu_c * theta_e * theta_e * sin(theta);
+    if (nu > 1.0e12 * nu_s) return 0.0;
+    const double x = nu / nu_s;
+    const double xp = cbrt(x);
+    const double xx = sqrt(x) + JNU_CST * sqrt(xp);
+    const double f = xx * xx;
+    return (kSqrt2 * kPi * EE * EE * n_e * nu_s / (3.0 * CL * k2)) * f * exp(-xp);
+}
+
+__device__ __forceinline__ double alpha_inv_scatt(const Params &P, double nu, double theta_e, double n_e) {
+    const double e_g = HPL * nu / (ME * CL * CL);
+    const double kappa = hotcross_lkup(P, e_g, theta_e) / MP;
+    return nu * kappa * n_e * MP;
+}
+
+__device__ __forceinline__ double alpha_inv_abs(const Params &P, double nu, double theta_e, double n_e, double b,
+                                                double theta) {
+    const double j = synch(P, nu, n_e, theta_e, b, theta) / (nu * nu);
+    const double x = HPL * nu / (ME * CL * CL * theta_e);
+    double b_nu;
+    if (x < 1.0e-3)
+        b_nu = (2.0 * HPL / (CL * CL)) / (x / 24.0 * (24.0 + x * (12.0 + x * (4.0 + x))));
+    else
+        b_nu = (2.0 * HPL / (CL * CL)) / (exp(x) - 1.0);
+    return j / (b_nu + 1.0e-100);
+}
+
+/* ------------------------------------------------------------------------- */
+/* scattering: tetrads.cpp:46-194, proba.cpp:30-215, harm_model.cpp:1071-1215 */
+/* ------------------------------------------------------------------------- */
+/* g(a, b) with the sparse MKS metric (zero entries skipped) */
+__device__ __forceinline__ double gdot(const Gcov &G, const double a[4], const double b[4]) {
+    return a[0] * (G.g00 * b[0] + G.g01 * b[1] + G.g03 * b[3]) + a[1] * (G.g01 * b[0] + G.g11 * b[1] + G.g13 * b[3]) +
+           a[2] * (G.g22 * b[2]) + a[3] * (G.g03 * b[0] + G.g13 * b[1] + G.g33 * b[3]);
+}
+
+__device__ __forceinline__ void t_normalize(double v[4], const Gcov &G) {
+    const double n = 1.0 / sqrt(fabs(gdot(G, v, v)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= n;
+}
+
+__device__ __forceinline__ void t_project_out(double va[4], const double vb[4], const Gcov &G) {
+    const double f = gdot(G, va, vb) / gdot(G, vb, vb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) va[i] -= vb[i] * f;
+}
+
+/* make_tetrad (tetrads.cpp:68-124): Gram-Schmidt of (u, trial, e2, e3) in g; returns e_con only,
+ * e_cov rows are lower(e_con) with row 0 negated and are formed on demand. */
+__device__ __forceinline__ void make_tetrad(const double u_con[4], double trial[4], const Gcov &G, double ec[4][4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ec[0][i] = u_con[i];
+    t_normalize(ec[0], G);
+    if (gdot(G, trial, trial) < 1.0e-30) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) trial[i] = (i == 1) ? 1.0 : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ec[1][i] = trial[i];
+    t_project_out(ec[1], ec[0], G);
+    t_normalize(ec[1], G);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ec[2][i] = (i == 2) ? 1.0 : 0.0;
+    t_project_out(ec[2], ec[0], G);
+    t_project_out(ec[2], ec[1], G);
+    t_normalize(ec[2], G);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ec[3][i] = (i == 3) ? 1.0 : 0.0;
+    t_project_out(ec[3], ec[0], G);
+    t_project_out(ec[3], ec[1], G);
+    t_project_out(ec[3], ec[2], G);
+    t_normalize(ec[3], G);
+}
+
+/* row i of e_cov = lower(e_con[i]) (row 0 negated) */
+__device__ __forceinline__ void tetrad_cov_row(const double ec[4][4], const Gcov &G, int i, double el[4]) {
+    lower(G, ec[i], el);
+    if (i == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) el[j] = -el[j];
+    }
+}
+
+__device__ __forceinline__ void boost(const double v[4], const double u[4], double vp[4]) {
+    const double g = u[0];
+    const double v_ = sqrt(fabs(1.0 - 1.0 / (g * g)));
+    const double ig = 1.0 / (g * v_ + EPS);
+    const double n1 = u[1] * ig, n2 = u[2] * ig, n3 = u[3] * ig;
+    const double gm1 = g - 1.0;
+    vp[0] = u[0] * v[0] - u[1] * v[1] - u[2] * v[2] - u[3] * v[3];
+    vp[1] = -u[1] * v[0] + (1.0 + n1 * n1 * gm1) * v[1] + n1 * n2 * gm1 * v[2] + n1 * n3 * gm1 * v[3];
+    vp[2] = -u[2] * v[0] + n2 * n1 * gm1 * v[1] + (1.0 + n2 * n2 * gm1) * v[2] + n2 * n3 * gm1 * v[3];
+    vp[3] = -u[3] * v[0] + n3 * n1 * gm1 * v[1] + n3 * n2 * gm1 * v[2] + (1.0 + n3 * n3 * gm1) * v[3];
+}
+
+__device__ __forceinline__ void sample_rand_dir(Rng &g, double &x, double &y, double &z) {
+    z = uniform(g) * 2.0 - 1.0;
+    const double phi = uniform(g) * 2.0 * kPi;
+    double s, c;
+    sincos(phi, &s, &c);
+    const double sq = sqrt(1.0 - z * z);
+    x = sq * c;
+    y = sq * s;
+}
+
+__device__ __forceinline__ double sample_y_distr(Rng &g, double theta_e) {
+    double pi_3 = sqrt(kPi) / 4.0;
+    double pi_4 = sqrt(0.5 * theta_e) / 2.0;
+    double pi_5 = 3.0 * sqrt(kPi) * theta_e / 8.0;
+    double pi_6 = theta_e * sqrt(0.5 * theta_e);
+    const double s_3 = pi_3 + pi_4 + pi_5 + pi_6;
+    pi_3 /= s_3;
+    pi_4 /= s_3;
+    pi_5 /= s_3;
+    double y, x2, prob;
+    do {
+        const double x1 = uniform(g);
+        int dof;
+        if (x1 < pi_3)
+            dof = 3;
+        else if (x1 < pi_3 + pi_4)
+            dof = 4;
+        else if (x1 < pi_3 + pi_4 + pi_5)
+            dof = 5;
+        else
+            dof = 6;
+        const double x = chi_sq(g, dof);
+        y = sqrt(x / 2.0);
+        x2 = uniform(g);
+        const double num = sqrt(1.0 + 0.5 * theta_e * y * y);
+        const double den = (1.0 + y * sqrt(0.5 * theta_e));
+        prob = num / den;
+    } while (x2 >= prob);
+    return y;
+}
+
+__device__ __forceinline__ void sample_electron(Rng &g, const double k[4], double p[4], double theta_e) {
+    double sigma_kn, gamma_e, beta_e, mu, x1;
+    do {
+        const double y = sample_y_distr(g, theta_e);
+        gamma_e = y * y * theta_e + 1.0;
+        beta_e = sqrt(1.0 - 1.0 / (gamma_e * gamma_e));
+        const double u = uniform(g);
+        const double det = 1.0 + 2.0 * beta_e + beta_e * beta_e - 4.0 * beta_e * u;
+        mu = (1.0 - sqrt(det)) / beta_e;
+        mu = fmin(fmax(mu, -1.0), 1.0);
+        const double k_ = gamma_e * (1.0 - beta_e * mu) * k[0];
+        if (k_ < 1.0e-3)
+            sigma_kn = 1.0 - 2.0 * k_;
+        else
+            sigma_kn = (3.0 / (4.0 * k_ * k_)) * (2.0 + k_ * k_ * (1.0 + k_) / ((1.0 + 2.0 * k_) * (1.0 + 2.0 * k_)) +
+                                                  (k_ * k_ - 2.0 * k_ - 2.0) / (2.0 * k_) * log(1.0 + 2.0 * k_));
+        x1 = uniform(g);
+    } while (x1 >= sigma_kn);
+    const double iv0 = 1.0 / sqrt(k[1] * k[1] + k[2] * k[2] + k[3] * k[3]);
+    const double v0x = k[1] * iv0, v0y = k[2] * iv0, v0z = k[3] * iv0;
+    double n0x, n0y, n0z;
+    sample_rand_dir(g, n0x, n0y, n0z);
+    const double n0dotv0 = v0x * n0x + v0y * n0y + v0z * n0z;
+    double v1x = n0x - n0dotv0 * v0x, v1y = n0y - n0dotv0 * v0y, v1z = n0z - n0dotv0 * v0z;
+    const double iv1 = 1.0 / sqrt(v1x * v1x + v1y * v1y + v1z * v1z);
+    v1x *= iv1;
+    v1y *= iv1;
+    v1z *= iv1;
+    const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
+    const double phi = uniform(g) * 2.0 * kPi;
+    double s_phi, c_phi;
+    sincos(phi, &s_phi, &c_phi);
+    const double c_th = mu, s_th = sqrt(1. - mu * mu);
+    const double gb = gamma_e * beta_e;
+    p[0] = gamma_e;
+    p[1] = gb * (c_th * v0x + s_th * (c_phi * v1x + s_phi * v2x));
+    p[2] = gb * (c_th * v0y + s_th * (c_phi * v1y + s_phi * v2y));
+    p[3] = gb * (c_th * v0z + s_th * (c_phi * v1z + s_phi * v2z));
+}
+
+__device__ __forceinline__ double sample_klein_nishina(Rng &g, double k0) {
+    const double k0pmin = k0 / (1.0 + 2.0 * k0), k0pmax = k0;
+    const double xmax = 2.0 * (1.0 + 2.0 * k0 + 2.0 * k0 * k0) / (k0 * k0 * (1.0 + 2.0 * k0));
+    double x1, kt;
+    while (true) {
+        kt = k0pmin + (k0pmax - k0pmin) * uniform(g);
+        x1 = xmax * uniform(g);
+        const double ch = 1.0 + 1.0 / k0 - 1.0 / kt;
+        const double kn = (k0 / kt + kt / k0 - 1.0 + ch * ch) / (k0 * k0);
+        if (!(x1 >= kn)) break;
+    }
+    return kt;
+}
+
+__device__ __forceinline__ double sample_thomson(Rng &g) {
+    double x1, x2;
+    do {
+        x1 = 2.0 * uniform(g) - 1.0;
+        x2 = (3.0 / 4.0) * uniform(g);
+    } while (x2 >= (3.0 / 8.0) * (1.0 + x1 * x1));
+    return x1;
+}
+
+__device__ __forceinline__ void sample_scattered(Rng &g, const double k[4], double p[4], double kp[4]) {
+    double ke[4];
+    boost(k, p, ke);
+    double k0p, c_th;
+    if (ke[0] > 1.0e-4) {
+        k0p = sample_klein_nishina(g, ke[0]);
+        c_th = 1.0 - 1.0 / k0p + 1.0 / ke[0];
+    } else {
+        k0p = ke[0];
+        c_th = sample_thomson(g);
+    }
+    const double s_th = sqrt(fabs(1.0 - c_th * c_th));
+    const double ik = 1.0 / ke[0];
+    const double v0x = ke[1] * ik, v0y = ke[2] * ik, v0z = ke[3] * ik;
+    double n0x, n0y, n0z;
+    sample_rand_dir(g, n0x, n0y, n0z);
+    const double n0dotv0 = v0x * n0x + v0y * n0y + v0z * n0z;
+    double v1x = n0x - n0dotv0 * v0x, v1y = n0y - n0dotv0 * v0y, v1z = n0z - n0dotv0 * v0z;
+    const double iv1 = 1.0 / sqrt(v1x * v1x + v1y * v1y + v1z * v1z);
+    v1x *= iv1;
+    v1y *= iv1;
+    v1z *= iv1;
+    const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
+    const double phi = 2.0 * kPi * uniform(g);
+    double s_phi, c_phi;
+    sincos(phi, &s_phi, &c_phi);
+    p[1] = -p[1];
+    p[2] = -p[2];
+    p[3] = -p[3];
+    const double d1 = c_th * v0x + s_th * (c_phi * v1x + s_phi * v2x);
+    const double d2 = c_th * v0y + s_th * (c_phi * v1y + s_phi * v2y);
+    const double d3 = c_th * v0z + s_th * (c_phi * v1z + s_phi * v2z);
+    const double kpe[4] = {k0p, k0p * d1, k0p * d2, k0p * d3};
+    boost(kpe, p, kp);
+}
+
+} /* namespace grm */

@@ -1,0 +1,1013 @@
+/*
+ * grm_engine.hip -- persistent-wavefront superphoton transport for MI355X (gfx950)
+ * and the C-ABI engine entry points (include/grmonty_amd.h).
+ *
+ * Replaces the reference's 2-stream x 16384-slot lock-step pipeline of nine kernels
+ * per geodesic step with host refills and host re-queueing of scattered photons
+ * (super_photon.cu:505-1037).  Here ONE kernel launch tracks a whole batch:
+ *
+ *   - each lane owns one superphoton in VGPRs for its whole life
+ *     (track_super_photon, harm_model.cpp:894-1069, CPU semantics);
+ *   - idle lanes refill first from their own child stack, then from the batch pool
+ *     with one wave-aggregated atomic per refill (ballot + popcount);
+ *   - a scattering pushes the child onto the lane's private stack in HBM (no
+ *     inter-lane synchronisation); a full stack spills to an overflow pool that
+ *     the host relaunches over (double-buffered) until empty;
+ *   - escaping photons are binned with fp64 global atomics (record_super_photon,
+ *     harm_model.cpp:1291-1335); counters are u64 (fixes SURVEY Q7).
+ *
+ * RNG: Philox4x32-10 stream per photon id (key = seed); a child's stream id is a
+ * function of its parent's id and draw counter, so results do not depend on lane
+ * assignment or scheduling (bias mode FROZEN makes a batch fully reproducible).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "grm_device.h"
+
+using namespace grm;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int MIN_WAVES_PER_SIMD = 2;
+constexpr int STACK_DEPTH = 8;
+
+/* 208-B scatter request: the state at a scattering event from which the child
+ * photon is sampled later (scatter_super_photon, harm_model.cpp:1071-1145).
+ * Lane stacks and overflow pools hold these. */
+struct alignas(16) SReq {
+    double x[4], k[4];          /* parent position / wave vector at the scattering point */
+    double u_con[4], b_con[4];  /* fluid 4-velocity and b^mu there */
+    double b, theta_e;          /* |B| (Gauss), Theta_e there */
+    double w;                   /* child weight w_parent / bias */
+    double n_e_0, theta_e_0, e_0;
+    uint64_t id, parent;        /* child stream id, parent stream id */
+    int32_t n_scatt, pad0;
+    double pad1;
+};
+static_assert(sizeof(SReq) == 208, "SReq layout");
+
+/* 80-B per-lane cold photon fields (touched only at birth, scattering and recording) */
+struct alignas(16) Cold {
+    double e, l, x1i, x2i, n_e_0, theta_e_0, b_0, e_0;
+    uint64_t parent;
+    double pad;
+};
+static_assert(sizeof(Cold) == 80, "Cold layout");
+
+struct DevCounters {
+    unsigned long long n_recorded, n_scatt, max_tau_bits, n_steps;
+    unsigned long long n_tracked, n_children, n_overflow, n_dropped;
+    unsigned long long n_primaries, pad[7];
+};
+
+struct Ctl {
+    const void *pool;      /* grm_init_photon[] (kind 0) or SReq[] (kind 1) */
+    int pool_kind;
+    unsigned long long n_pool;
+    unsigned long long *pool_head;
+    uint64_t id_base;
+    uint32_t key0, key1;
+    SReq *stack;           /* [lanes][STACK_DEPTH] */
+    Cold *cold;            /* [lanes] */
+    SReq *ovf;             /* overflow out */
+    unsigned long long ovf_cap;
+    unsigned long long *ovf_count;
+    grm_spectrum_cell *spec;
+    DevCounters *ctr;
+    grm_trace *trace;
+    unsigned long long trace_cap;
+    unsigned long long *trace_count;
+    int bias_frozen;
+    double f_scatt, f_rec, f_maxtau;
+};
+
+/* hot photon state: lives in VGPRs for the photon's whole life */
+struct Lane {
+    double x[4], k[4], dk[4];
+    double w, e_0_s, tau_abs, tau_scatt;
+    double alpha_scatti, alpha_absi, bi, fl_ne;
+    int n_scatt, n_step;
+    Rng rng;
+};
+
+__device__ __forceinline__ double bias_func(const Params &P, const Ctl &C, double t_e, double w) {
+    double scatt, rec, mts;
+    if (C.bias_frozen) {
+        scatt = C.f_scatt;
+        rec = C.f_rec;
+        mts = C.f_maxtau;
+    } else { /* live, reference-like adaptive bias (harm_model.cpp:1391-1404) */
+        scatt = (double)__hip_atomic_load(&C.ctr->n_scatt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rec = (double)__hip_atomic_load(&C.ctr->n_recorded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mts = __longlong_as_double(
+            (long long)__hip_atomic_load(&C.ctr->max_tau_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    const double max = 0.5 * w / WEIGHT_MIN;
+    const double avg = scatt / (1.0 * rec + 1.0);
+    double bias = 100.0 * t_e * t_e / (P.bias_norm * mts * (avg + 2.0));
+    if (bias < TP_OVER_TE) bias = TP_OVER_TE;
+    if (bias > max) bias = max;
+    return bias / TP_OVER_TE;
+}
+
+/* stop_criterion (harm_model.cpp:1589-1616) */
+__device__ __forceinline__ bool stop_criterion(const Params &P, Lane &L) {
+    if (L.x[1] < P.x1_min) return true;
+    if (L.x[1] > P.x1_max) {
+        if (L.w < WEIGHT_MIN) {
+            if (uniform(L.rng) <= 1.0 / ROULETTE)
+                L.w *= ROULETTE;
+            else
+                L.w = 0.0;
+        }
+        return true;
+    }
+    if (L.w < WEIGHT_MIN) {
+        if (uniform(L.rng) <= 1.0 / ROULETTE) {
+            L.w *= ROULETTE;
+        } else {
+            L.w = 0.0;
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ void write_trace(const Ctl &C, const Cold *cold, uint64_t id, double w, double x1, double x2,
+                                         double x3, double tau_abs, double tau_scatt, int n_scatt, int n_step,
+                                         int reason, int ix2, int i_e) {
+    const unsigned long long t = atomicAdd(C.trace_count, 1ull);
+    if (t >= C.trace_cap) return;
+    grm_trace &r = C.trace[t];
+    r.id = id;
+    r.parent_id = cold ? cold->parent : ~0ull;
+    r.w = w;
+    r.e = cold ? cold->e : 0.0;
+    r.x1 = x1;
+    r.x2 = x2;
+    r.x3 = x3;
+    r.tau_abs = tau_abs;
+    r.tau_scatt = tau_scatt;
+    r.n_scatt = n_scatt;
+    r.n_step = n_step;
+    r.end_reason = reason;
+    r.ix2 = ix2;
+    r.i_e = i_e;
+    r.pad_ = 0;
+}
+
+__device__ __forceinline__ void trace_end(const Ctl &C, const Cold *cold, const Lane &L, int reason) {
+    if (C.trace)
+        write_trace(C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs, L.tau_scatt, L.n_scatt, L.n_step,
+                    reason, -1, -1);
+}
+
+/* record_super_photon (harm_model.cpp:1291-1335) */
+__device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, uint64_t id, double w, double x1,
+                              double x2, double x3, double tau_abs, double tau_scatt, int n_scatt, int n_step) {
+    int ix2 = -1, i_e = -1, reason = 1;
+    const double e = cold->e;
+    if (!(isnan(w) || isnan(e))) {
+        if (tau_scatt > __longlong_as_double((long long)C.ctr->max_tau_bits))
+            atomicMax(&C.ctr->max_tau_bits, (unsigned long long)__double_as_longlong(tau_scatt));
+        if (x2 < 0.5 * (P.xs2 + P.xe2))
+            ix2 = (int)(x2 / P.th_dx2);
+        else
+            ix2 = (int)((P.xe2 - x2) / P.th_dx2);
+        if (ix2 >= 0 && ix2 < N_TH_BINS) {
+            i_e = (int)((log(e) - P.spec_l_e_0) / SPEC_D_L_E + 2.5) - 2;
+            if (i_e >= 0 && i_e < N_E_BINS) {
+                reason = 0;
+                atomicAdd(&C.ctr->n_recorded, 1ull);
+                atomicAdd(&C.ctr->n_scatt, (unsigned long long)n_scatt);
+                grm_spectrum_cell *s = C.spec + ix2 * N_E_BINS + i_e;
+                const double x1i = cold->x1i, x2i = cold->x2i;
+                unsafeAtomicAdd(&s->dn_dle, w);
+                unsafeAtomicAdd(&s->de_dle, w * e);
+                unsafeAtomicAdd(&s->tau_abs, w * tau_abs);
+                unsafeAtomicAdd(&s->tau_scatt, w * tau_scatt);
+                unsafeAtomicAdd(&s->x1i_av, w * x1i);
+                unsafeAtomicAdd(&s->x2i_sq, w * (x2i * x2i));
+                unsafeAtomicAdd(&s->x3f_sq, w * (x3 * x3));
+                unsafeAtomicAdd(&s->ne_0, w * cold->n_e_0);
+                unsafeAtomicAdd(&s->b_0, w * cold->b_0);
+                unsafeAtomicAdd(&s->theta_e_0, w * cold->theta_e_0);
+                unsafeAtomicAdd(&s->nscatt, (double)n_scatt);
+                unsafeAtomicAdd(&s->nph, 1.0);
+            } else {
+                i_e = -1;
+            }
+        } else {
+            ix2 = -1;
+        }
+    }
+    if (C.trace)
+        write_trace(C, cold, id, w, x1, x2, x3, tau_abs, tau_scatt, n_scatt, n_step, reason, ix2, i_e);
+}
+
+__device__ __forceinline__ void end_of_life(const Params &P, const Ctl &C, const Cold *cold, const Lane &L) {
+    /* record_criterion (harm_model.cpp:1618) && n_step <= max_n_step (:1066) */
+    if (L.x[1] > P.x1_max && L.n_step <= MAX_N_STEP)
+        record_photon(P, C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs, L.tau_scatt, L.n_scatt, L.n_step);
+    else
+        trace_end(C, cold, L, 2);
+}
+
+/* photon set-up at the head of track_super_photon (harm_model.cpp:895-917). false = invalid */
+__device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lane &L) {
+    if (isnan(L.x[0]) || isnan(L.x[1]) || isnan(L.x[2]) || isnan(L.x[3]) || isnan(L.k[0]) || isnan(L.k[1]) ||
+        isnan(L.k[2]) || isnan(L.k[3]) || L.w == 0.0) {
+        trace_end(C, cold, L, 4);
+        return false;
+    }
+    Trig T;
+    trig_at(P, L.x, T);
+    Gcov G;
+    gcov_from_trig(P, T, G);
+    Fluid F;
+    fluid_params(P, L.x, G, F);
+    const double theta = bk_angle(L.k, F, P.b_unit);
+    const double nu = fluid_nu(L.k, F);
+    L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
+    L.alpha_absi = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
+    L.bi = bias_func(P, C, F.theta_e, L.w);
+    L.fl_ne = F.n_e;
+    Conn Cn;
+    connection(P, T, Cn);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L.dk[i] = geo_rhs(Cn, i, L.k);
+    L.n_step = 0;
+    L.tau_abs = L.tau_scatt = 0.0;
+    L.e_0_s = cold->e;
+    return true;
+}
+
+/* emitted photon -> lane (harm_model.cpp:373-391) */
+__device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L, Cold *cold) {
+    const double2 *s = reinterpret_cast<const double2 *>(reinterpret_cast<const grm_init_photon *>(C.pool) + idx);
+    double2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = s[q];
+    L.x[0] = v[0].x; L.x[1] = v[0].y; L.x[2] = v[1].x; L.x[3] = v[1].y;
+    L.k[0] = v[2].x; L.k[1] = v[2].y; L.k[2] = v[3].x; L.k[3] = v[3].y;
+    L.w = v[4].x;
+    L.n_scatt = 0;
+    L.rng.id = C.id_base + idx;
+    L.rng.ctr = 0;
+    Cold c;
+    c.e = v[4].y;
+    c.l = v[5].x;
+    c.x1i = L.x[1];
+    c.x2i = L.x[2];
+    c.n_e_0 = v[5].y;
+    c.theta_e_0 = v[6].x;
+    c.b_0 = v[6].y;
+    c.e_0 = v[7].x;
+    c.parent = ~0ull;
+    c.pad = 0.0;
+    *cold = c;
+}
+
+/* scatter request -> child photon in the lane (scatter_super_photon after its first
+ * validity check, harm_model.cpp:1083-1144, with sample_scattered_photon :1147-1215).
+ * false = child invalid (k_tetrad out of range or NaN). */
+__device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane &L, Cold *cold) {
+    L.rng.id = R.id;
+    L.rng.ctr = 0;
+    L.w = R.w;
+    L.n_scatt = R.n_scatt;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L.x[i] = R.x[i];
+    Cold c;
+    c.x1i = R.x[1];
+    c.x2i = R.x[2];
+    c.n_e_0 = R.n_e_0;
+    c.theta_e_0 = R.theta_e_0;
+    c.b_0 = R.b;
+    c.e_0 = R.e_0;
+    c.parent = R.parent;
+    c.e = 0.0;
+    c.l = 0.0;
+    c.pad = 0.0;
+    Trig T;
+    trig_at(P, R.x, T);
+    Gcov G;
+    gcov_from_trig(P, T, G);
+    double bh[4];
+    if (R.b > 0.0) {
+        const double s = R.b / P.b_unit;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bh[i] = R.b_con[i] / s;
+    } else {
+        bh[0] = 0.0; bh[1] = 1.0; bh[2] = 0.0; bh[3] = 0.0;
+    }
+    double ec[4][4];
+    make_tetrad(R.u_con, bh, G, ec);
+    double kt[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double el[4];
+        tetrad_cov_row(ec, G, i, el);
+        kt[i] = el[0] * R.k[0] + el[1] * R.k[1] + el[2] * R.k[2] + el[3] * R.k[3];
+    }
+    bool ok = !(kt[0] > 1.0e5 || kt[0] < 0.0 || isnan(kt[1]));
+    if (ok) {
+        double p[4], ktp[4];
+        sample_electron(L.rng, kt, p, R.theta_e);
+        sample_scattered(L.rng, kt, p, ktp);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) L.k[i] = ec[0][i] * ktp[0] + ec[1][i] * ktp[1] + ec[2][i] * ktp[2] + ec[3][i] * ktp[3];
+        ok = !isnan(L.k[1]);
+        if (ok) {
+            /* e_cov^T (-k0', k1', k2', k3'): only components 0 and 3 are needed (e, l) */
+            ktp[0] = -ktp[0];
+            double t0 = 0.0, t3 = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double el[4];
+                tetrad_cov_row(ec, G, j, el);
+                t0 += el[0] * ktp[j];
+                t3 += el[3] * ktp[j];
+            }
+            c.e = -t0;
+            c.l = t3;
+        }
+    }
+    *cold = c;
+    return ok;
+}
+
+__device__ __forceinline__ void load_sreq(const SReq *src, SReq &R) {
+    const double2 *s = reinterpret_cast<const double2 *>(src);
+    double2 *d = reinterpret_cast<double2 *>(&R);
+#pragma unroll
+    for (int q = 0; q < 13; ++q) d[q] = s[q];
+}
+
+__device__ __forceinline__ void store_sreq(SReq *dst, const SReq &R) {
+    const double2 *s = reinterpret_cast<const double2 *>(&R);
+    double2 *d = reinterpret_cast<double2 *>(dst);
+#pragma unroll
+    for (int q = 0; q < 13; ++q) d[q] = s[q];
+}
+
+/* one iteration of the while loop of track_super_photon (harm_model.cpp:919-1063).
+ * returns false when the photon's life ended. */
+__device__ bool transport_step(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *my_stack, int &sdepth,
+                               unsigned long long &steps, const Slot &ph2, const Slot &bk) {
+    if (stop_criterion(P, L)) {
+        end_of_life(P, C, cold, L);
+        return false;
+    }
+    /* photon_2 (harm_model.cpp:920-925): only read back if this step scatters -> LDS */
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ph2[i] = L.x[i];
+        ph2[4 + i] = L.k[i];
+        ph2[8 + i] = L.dk[i];
+    }
+    ph2[12] = L.e_0_s;
+    const double dl = step_size(P, L.x, L.k);
+    push_photon(P, L.x, L.k, L.dk, L.e_0_s, dl, bk);
+    ++steps;
+    if (stop_criterion(P, L)) {
+        end_of_life(P, C, cold, L);
+        return false;
+    }
+    if (L.alpha_absi > 0.0 || L.alpha_scatti > 0.0 || L.fl_ne > 0.0) {
+        Trig T;
+        trig_at(P, L.x, T);
+        Gcov G;
+        gcov_from_trig(P, T, G);
+        Fluid F;
+        fluid_params(P, L.x, G, F);
+        L.fl_ne = F.n_e;
+        const bool bound_flag = F.n_e == 0.0;
+        double theta = 0.0, nu = 0.0;
+        if (!bound_flag) {
+            theta = bk_angle(L.k, F, P.b_unit);
+            nu = fluid_nu(L.k, F);
+        }
+        double d_tau_scatt, d_tau_abs, bias;
+        if (bound_flag || nu < 0.0) {
+            d_tau_scatt = 0.5 * L.alpha_scatti * P.d_tau_k * dl;
+            d_tau_abs = 0.5 * L.alpha_absi * P.d_tau_k * dl;
+            L.alpha_scatti = 0.0;
+            L.alpha_absi = 0.0;
+            bias = 0.0;
+            L.bi = 0.0;
+        } else {
+            const double a_sf = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
+            d_tau_scatt = 0.5 * (L.alpha_scatti + a_sf) * P.d_tau_k * dl;
+            L.alpha_scatti = a_sf;
+            const double a_af = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
+            d_tau_abs = 0.5 * (L.alpha_absi + a_af) * P.d_tau_k * dl;
+            L.alpha_absi = a_af;
+            const double bf = bias_func(P, C, F.theta_e, L.w);
+            bias = 0.5 * (L.bi + bf);
+            L.bi = bf;
+        }
+        const double x1 = -log(uniform(L.rng));
+        const double wc = L.w / bias;
+        if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) {
+            const double frac = x1 / (bias * d_tau_scatt);
+            d_tau_abs *= frac;
+            if (d_tau_abs > 100) {
+                trace_end(C, cold, L, 2);
+                return false; /* absorbed before scattering */
+            }
+            d_tau_scatt *= frac;
+            const double d_tau = d_tau_abs + d_tau_scatt;
+            if (d_tau_abs < 1.0e-3)
+                L.w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+            else
+                L.w *= exp(-d_tau);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                L.x[i] = ph2[i];
+                L.k[i] = ph2[4 + i];
+                L.dk[i] = ph2[8 + i];
+            }
+            L.e_0_s = ph2[12];
+            push_photon(P, L.x, L.k, L.dk, L.e_0_s, dl * frac, bk);
+            trig_at(P, L.x, T);
+            gcov_from_trig(P, T, G);
+            fluid_params(P, L.x, G, F);
+            L.fl_ne = F.n_e;
+            if (F.n_e > 0.0) {
+                /* scatter_super_photon's parent-side check (:1076-1081) */
+                if (L.k[0] > 1.0e5 || L.k[0] < 0.0 || isnan(L.k[0]) || isnan(L.k[1]) || isnan(L.k[3])) {
+                    L.k[0] = fabs(L.k[0]);
+                    L.w = 0.0;
+                    trace_end(C, cold, L, 2);
+                    return false;
+                }
+                /* defer the child's sampling: push a scatter request (its stream id is fixed now) */
+                SReq R;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    R.x[i] = L.x[i];
+                    R.k[i] = L.k[i];
+                    R.u_con[i] = F.u_con[i];
+                    R.b_con[i] = F.b_con[i];
+                }
+                R.b = F.b;
+                R.theta_e = F.theta_e;
+                R.w = wc;
+                R.n_e_0 = cold->n_e_0;
+                R.theta_e_0 = cold->theta_e_0;
+                R.e_0 = cold->e_0;
+                R.id = child_id(L.rng.id, L.rng.ctr);
+                R.parent = L.rng.id;
+                R.n_scatt = L.n_scatt + 1;
+                R.pad0 = 0;
+                R.pad1 = 0.0;
+                atomicAdd(&C.ctr->n_children, 1ull);
+                if (sdepth < STACK_DEPTH) {
+                    store_sreq(my_stack + sdepth, R);
+                    ++sdepth;
+                } else {
+                    const unsigned long long o = atomicAdd(C.ovf_count, 1ull);
+                    if (o < C.ovf_cap)
+                        store_sreq(C.ovf + o, R);
+                    else
+                        atomicAdd(&C.ctr->n_dropped, 1ull);
+                    atomicAdd(&C.ctr->n_overflow, 1ull);
+                }
+            }
+            theta = bk_angle(L.k, F, P.b_unit);
+            nu = fluid_nu(L.k, F);
+            if (nu < 0.0) {
+                L.alpha_scatti = 0.0;
+                L.alpha_absi = 0.0;
+            } else {
+                L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
+                L.alpha_absi = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
+            }
+            L.bi = bias_func(P, C, F.theta_e, L.w);
+        } else {
+            if (d_tau_abs > 100) {
+                trace_end(C, cold, L, 2);
+                return false; /* absorbed */
+            }
+            const double d_tau = d_tau_abs + d_tau_scatt;
+            if (d_tau < 1.0e-3)
+                L.w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
+            else
+                L.w *= exp(-d_tau);
+        }
+        L.tau_abs += d_tau_abs;
+        L.tau_scatt += d_tau_scatt;
+    }
+    ++L.n_step;
+    if (L.n_step > MAX_N_STEP) {
+        trace_end(C, cold, L, 3);
+        return false;
+    }
+    return true;
+}
+
+/* LDS per lane: photon_2 (13 doubles) + push backup (12 doubles), [slot][lane] */
+constexpr int LDS_DOUBLES_PER_LANE = 25;
+
+__global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P, Ctl C) {
+    __shared__ double lds[LDS_DOUBLES_PER_LANE * BLOCK];
+    const Slot ph2{lds + threadIdx.x, BLOCK};
+    const Slot bk{lds + 13 * BLOCK + threadIdx.x, BLOCK};
+    const unsigned lane_id = threadIdx.x & 63;
+    const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    SReq *my_stack = C.stack + gtid * STACK_DEPTH;
+    Cold *cold = C.cold + gtid;
+    Lane L;
+    L.rng.k0 = C.key0;
+    L.rng.k1 = C.key1;
+    bool active = false;
+    bool pool_done = false; /* wave-uniform */
+    int sdepth = 0;
+    unsigned long long steps = 0, tracked = 0, primaries = 0;
+    const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
+
+    while (true) {
+        /* refill, children first: pop a scatter request and sample the child */
+        if (!active && sdepth > 0) {
+            --sdepth;
+            SReq R;
+            load_sreq(my_stack + sdepth, R);
+            if (sample_child(P, C, R, L, cold)) {
+                active = init_photon(P, C, cold, L);
+            } else if (C.trace) {
+                write_trace(C, cold, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4, -1, -1);
+            }
+            ++tracked;
+        }
+        /* then the shared pool: one atomic per wave */
+        const bool want = !active && !pool_done;
+        const unsigned long long mask = __ballot(want);
+        if (mask) {
+            const int cnt = __popcll(mask);
+            const int leader = __ffsll((long long)mask) - 1;
+            unsigned long long base = 0;
+            if ((int)lane_id == leader) base = atomicAdd(C.pool_head, (unsigned long long)cnt);
+            base = __shfl(base, leader);
+            if (base + cnt >= C.n_pool) pool_done = true;
+            if (want) {
+                const unsigned long long idx = base + __popcll(mask & lt_mask);
+                if (idx < C.n_pool) {
+                    bool ok = true;
+                    if (C.pool_kind == 0) {
+                        load_primary(C, idx, L, cold);
+                        ++primaries;
+                    } else {
+                        SReq R;
+                        load_sreq(reinterpret_cast<const SReq *>(C.pool) + idx, R);
+                        ok = sample_child(P, C, R, L, cold);
+                        if (!ok && C.trace)
+                            write_trace(C, cold, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4, -1, -1);
+                    }
+                    if (ok) active = init_photon(P, C, cold, L);
+                    ++tracked;
+                }
+            }
+        }
+        if (!__any(active)) {
+            if (pool_done && !__any(sdepth > 0)) break;
+            continue;
+        }
+        if (active) active = transport_step(P, C, L, cold, my_stack, sdepth, steps, ph2, bk);
+    }
+    /* wave-reduce the lane counters, one atomic per wave */
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        steps += __shfl_xor(steps, off);
+        tracked += __shfl_xor(tracked, off);
+        primaries += __shfl_xor(primaries, off);
+    }
+    if (lane_id == 0) {
+        atomicAdd(&C.ctr->n_steps, steps);
+        atomicAdd(&C.ctr->n_tracked, tracked);
+        atomicAdd(&C.ctr->n_primaries, primaries);
+    }
+}
+
+} /* namespace */
+
+/* ========================================================================= */
+/* engine object + C ABI                                                      */
+/* ========================================================================= */
+struct grm_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    Params P{};
+    double *d_zones = nullptr, *d_hot = nullptr, *d_k2 = nullptr;
+    DevCounters *d_ctr = nullptr;
+    grm_spectrum_cell *d_spec = nullptr;
+    SReq *d_stack = nullptr;
+    Cold *d_cold = nullptr;
+    size_t lanes = 0;
+    int grid = 0;
+    SReq *d_ovf[2] = {nullptr, nullptr};
+    unsigned long long ovf_cap = 0;
+    unsigned long long *d_small = nullptr; /* [0] pool head, [1..2] ovf counts, [3] trace count */
+    grm_init_photon *d_batch = nullptr;
+    size_t batch_cap = 0;
+    grm_trace *d_trace = nullptr;
+    unsigned long long trace_cap = 0;
+    uint64_t seed = 123;
+    int bias_mode = 0;
+    uint64_t id_base = 0;
+    int grid_override = 0;
+    double max_tau_init = 0.0;
+    bool frozen_set = false;
+    int64_t warmup = -1;     /* photons; -1 = lanes */
+    uint64_t history = 0;    /* primaries tracked since reset */
+    double fz_scatt = 0.0, fz_rec = 0.0, fz_maxtau = 0.0;
+    grm_stats stats{};
+    std::string err;
+};
+
+namespace {
+
+bool hip_ok(grm_engine *e, hipError_t st, const char *what) {
+    if (st == hipSuccess) return true;
+    if (e) e->err = std::string(what) + ": " + hipGetErrorString(st);
+    return false;
+}
+
+#define HIPCHK(e, call)                                   \
+    do {                                                  \
+        if (!hip_ok((e), (call), #call)) return -1;       \
+    } while (0)
+
+int alloc_lanes(grm_engine *e) {
+    int n_cu = 0;
+    HIPCHK(e, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
+    int per_cu = 0;
+    HIPCHK(e, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, track_kernel, BLOCK, 0));
+    if (per_cu < 1) per_cu = 1;
+    int grid = e->grid_override > 0 ? e->grid_override : n_cu * per_cu;
+    if (grid < 1) grid = 1;
+    const size_t lanes = (size_t)grid * BLOCK;
+    if (lanes != e->lanes) {
+        if (e->d_stack) (void)hipFree(e->d_stack);
+        if (e->d_cold) (void)hipFree(e->d_cold);
+        e->d_stack = nullptr;
+        e->d_cold = nullptr;
+        HIPCHK(e, hipMalloc(&e->d_stack, lanes * STACK_DEPTH * sizeof(SReq)));
+        HIPCHK(e, hipMalloc(&e->d_cold, lanes * sizeof(Cold)));
+        e->lanes = lanes;
+    }
+    e->grid = grid;
+    return 0;
+}
+
+int ensure_ovf(grm_engine *e, unsigned long long cap) {
+    if (cap <= e->ovf_cap) return 0;
+    for (int i = 0; i < 2; ++i) {
+        if (e->d_ovf[i]) hipFree(e->d_ovf[i]);
+        e->d_ovf[i] = nullptr;
+        HIPCHK(e, hipMalloc(&e->d_ovf[i], cap * sizeof(SReq)));
+    }
+    e->ovf_cap = cap;
+    return 0;
+}
+
+int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
+    if (n == 0) return 0;
+    /* overflow pool: children rarely spill (8-deep lane stacks); size ~ max(1M, n/4) */
+    if (ensure_ovf(e, std::max<unsigned long long>(1ull << 20, n / 4))) return -1;
+    Ctl C{};
+    C.pool = d_batch;
+    C.pool_kind = 0;
+    C.n_pool = n;
+    C.pool_head = e->d_small + 0;
+    C.id_base = e->id_base;
+    C.key0 = (uint32_t)e->seed;
+    C.key1 = (uint32_t)(e->seed >> 32);
+    C.stack = e->d_stack;
+    C.cold = e->d_cold;
+    C.ovf_cap = e->ovf_cap;
+    C.spec = e->d_spec;
+    C.ctr = e->d_ctr;
+    C.trace = e->trace_cap ? e->d_trace : nullptr;
+    C.trace_cap = e->trace_cap;
+    C.trace_count = e->d_small + 3;
+    C.bias_frozen = e->bias_mode;
+    if (e->bias_mode && e->frozen_set) {
+        C.f_scatt = e->fz_scatt;
+        C.f_rec = e->fz_rec;
+        C.f_maxtau = e->fz_maxtau;
+    } else if (e->bias_mode) {
+        DevCounters h;
+        HIPCHK(e, hipMemcpyAsync(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        C.f_scatt = (double)h.n_scatt;
+        C.f_rec = (double)h.n_recorded;
+        double mt;
+        std::memcpy(&mt, &h.max_tau_bits, sizeof(mt));
+        C.f_maxtau = mt;
+    }
+    unsigned long long steps_before = 0;
+    {
+        DevCounters h;
+        HIPCHK(e, hipMemcpy(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+        steps_before = h.n_steps;
+    }
+    double ms_total = 0.0;
+    int src = -1, dst = 0;
+    unsigned long long n_pool = n;
+    for (int pass = 0; n_pool > 0; ++pass) {
+        HIPCHK(e, hipMemsetAsync(e->d_small, 0, 3 * sizeof(unsigned long long), e->stream));
+        C.ovf = e->d_ovf[dst];
+        C.ovf_count = e->d_small + 1 + dst;
+        if (pass > 0) {
+            C.pool = e->d_ovf[src];
+            C.pool_kind = 1;
+            C.n_pool = n_pool;
+        }
+        HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+        hipLaunchKernelGGL(track_kernel, dim3(e->grid), dim3(BLOCK), 0, e->stream, e->P, C);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+        unsigned long long cnt = 0;
+        HIPCHK(e, hipMemcpyAsync(&cnt, C.ovf_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        float ms = 0.f;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+        ms_total += ms;
+        e->stats.n_launches++;
+        n_pool = std::min(cnt, e->ovf_cap);
+        src = dst;
+        dst ^= 1;
+        if (pass > 64) {
+            e->err = "overflow relaunch did not converge";
+            return -1;
+        }
+    }
+    DevCounters h;
+    HIPCHK(e, hipMemcpy(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+    e->stats.kernel_ms += ms_total;
+    e->stats.last_kernel_ms += ms_total;
+    e->stats.last_steps += h.n_steps - steps_before;
+    e->id_base += n;
+    e->history += n;
+    return 0;
+}
+
+/* one transport call: with live bias, the first photons after a reset go in launches that
+ * double the tracked history (64, 64, 128, ...) so that the adaptive bias of
+ * harm_model.cpp:1391-1404 sees counters close to the serial reference's; afterwards a single
+ * persistent launch updates them live. */
+int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
+    if (alloc_lanes(e)) return -1;
+    e->stats.last_kernel_ms = 0.0;
+    e->stats.last_steps = 0;
+    const uint64_t limit = e->warmup < 0 ? (uint64_t)e->lanes : (uint64_t)e->warmup;
+    size_t done = 0;
+    while (done < n) {
+        size_t sub = n - done;
+        if (!e->bias_mode && e->history < limit)
+            sub = std::min<size_t>(sub, std::max<uint64_t>(64, std::min<uint64_t>(e->history, limit - e->history)));
+        if (run_passes(e, d_batch + done, sub)) return -1;
+        done += sub;
+    }
+    return 0;
+}
+
+int reset_counters(grm_engine *e) {
+    HIPCHK(e, hipMemsetAsync(e->d_spec, 0, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS, e->stream));
+    DevCounters h;
+    std::memset(&h, 0, sizeof(h));
+    std::memcpy(&h.max_tau_bits, &e->max_tau_init, sizeof(double));
+    HIPCHK(e, hipMemcpyAsync(e->d_ctr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_small, 0, 4 * sizeof(unsigned long long), e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+} /* namespace */
+
+/* probe entry point lives in grm_probe.hip */
+extern "C" int grm_probe_impl(const Params &P, hipStream_t s, int which, const double *in, int in_stride, double *out,
+                              int out_stride, size_t n, std::string &err);
+
+extern "C" {
+
+int grm_engine_create(const grm_header *h, const double *const fields[8], const grm_units *u, const double *hotcross,
+                      const double *k2, const double scalars[4], int device, grm_engine **out) {
+    if (!h || !fields || !u || !hotcross || !k2 || !scalars || !out) return -1;
+    *out = nullptr;
+    if (h->n[0] < 2 || h->n[1] < 2) return -2;
+    grm_engine *e = new grm_engine();
+    e->device = device;
+    auto fail = [&](void) {
+        *out = e; /* hand back for last_error; caller destroys */
+        return -1;
+    };
+    if (!hip_ok(e, hipSetDevice(device), "hipSetDevice")) return fail();
+    if (!hip_ok(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking), "stream")) return fail();
+    if (!hip_ok(e, hipEventCreate(&e->ev0), "event") || !hip_ok(e, hipEventCreate(&e->ev1), "event")) return fail();
+    const size_t nz = (size_t)h->n[0] * h->n[1];
+    std::vector<double> zones(nz * 8);
+    for (size_t z = 0; z < nz; ++z)
+        for (int f = 0; f < 8; ++f) zones[z * 8 + f] = fields[f][z];
+    const size_t nhot = (size_t)(GRM_HC_N_W + 1) * (GRM_HC_N_T + 1);
+    if (!hip_ok(e, hipMalloc(&e->d_zones, nz * 8 * sizeof(double)), "zones") ||
+        !hip_ok(e, hipMalloc(&e->d_hot, nhot * sizeof(double)), "hotcross") ||
+        !hip_ok(e, hipMalloc(&e->d_k2, (GRM_N_E_SAMP + 1) * sizeof(double)), "k2") ||
+        !hip_ok(e, hipMalloc(&e->d_ctr, sizeof(DevCounters)), "counters") ||
+        !hip_ok(e, hipMalloc(&e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS), "spectrum") ||
+        !hip_ok(e, hipMalloc(&e->d_small, 8 * sizeof(unsigned long long)), "small"))
+        return fail();
+    if (!hip_ok(e, hipMemcpy(e->d_zones, zones.data(), nz * 8 * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
+        !hip_ok(e, hipMemcpy(e->d_hot, hotcross, nhot * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
+        !hip_ok(e, hipMemcpy(e->d_k2, k2, (GRM_N_E_SAMP + 1) * sizeof(double), hipMemcpyHostToDevice), "H2D"))
+        return fail();
+    Params &P = e->P;
+    P.n1 = h->n[0];
+    P.n2 = h->n[1];
+    P.xs1 = h->x_start[1];
+    P.xs2 = h->x_start[2];
+    P.xe1 = h->x_stop[1];
+    P.xe2 = h->x_stop[2];
+    P.dx1 = h->dx[1];
+    P.dx2 = h->dx[2];
+    P.a = h->a;
+    P.h_slope = h->h_slope;
+    P.r0 = h->r_0;
+    P.n_e_unit = u->n_e_unit;
+    P.theta_e_unit = u->theta_e_unit;
+    P.b_unit = u->b_unit;
+    P.bias_norm = scalars[0];
+    P.x1_min = scalars[1];
+    e->max_tau_init = scalars[2];
+    P.d_tau_k = scalars[3];
+    /* derived table constants, host libm (consts.hpp:33-157) */
+    P.x1_max = std::log(100.0);
+    P.hc_l_min_w = std::log10(1.0e-12);
+    P.hc_l_min_t = std::log10(1.0e-4);
+    P.hc_d_l_w = std::log10(1.0e6 / 1.0e-12) / GRM_HC_N_W;
+    P.hc_d_l_t = std::log10(1.0e4 / 1.0e-4) / GRM_HC_N_T;
+    P.jnu_l_min_t = std::log(0.3);
+    P.jnu_d_l_t = std::log(1.0e2 / 0.3) / GRM_N_E_SAMP;
+    P.spec_l_e_0 = std::log(1.0e-12);
+    P.th_dx2 = (h->x_stop[2] - h->x_start[2]) / (2.0 * N_TH_BINS);
+    P.zones = e->d_zones;
+    P.hotcross = e->d_hot;
+    P.k2 = e->d_k2;
+    if (reset_counters(e)) return fail();
+    *out = e;
+    return 0;
+}
+
+void grm_engine_destroy(grm_engine *e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    if (e->stream) hipStreamSynchronize(e->stream);
+    hipFree(e->d_zones);
+    hipFree(e->d_hot);
+    hipFree(e->d_k2);
+    hipFree(e->d_ctr);
+    hipFree(e->d_spec);
+    hipFree(e->d_stack);
+    hipFree(e->d_cold);
+    hipFree(e->d_ovf[0]);
+    hipFree(e->d_ovf[1]);
+    hipFree(e->d_small);
+    hipFree(e->d_batch);
+    hipFree(e->d_trace);
+    if (e->ev0) hipEventDestroy(e->ev0);
+    if (e->ev1) hipEventDestroy(e->ev1);
+    if (e->stream) hipStreamDestroy(e->stream);
+    delete e;
+}
+
+const char *grm_engine_last_error(const grm_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
+    if (!e) return -1;
+    hipSetDevice(e->device);
+    switch (opt) {
+    case GRM_OPT_SEED: e->seed = (uint64_t)v; return 0;
+    case GRM_OPT_BIAS_MODE: e->bias_mode = v ? 1 : 0; return 0;
+    case GRM_OPT_TRACE_CAP:
+        if (e->d_trace) hipFree(e->d_trace);
+        e->d_trace = nullptr;
+        e->trace_cap = 0;
+        if (v > 0) {
+            HIPCHK(e, hipMalloc(&e->d_trace, (size_t)v * sizeof(grm_trace)));
+            e->trace_cap = (unsigned long long)v;
+        }
+        return 0;
+    case GRM_OPT_GRID_BLOCKS: e->grid_override = (int)v; return 0;
+    case GRM_OPT_ID_BASE: e->id_base = (uint64_t)v; return 0;
+    case GRM_OPT_FROZEN_SCATT: e->fz_scatt = (double)v; e->frozen_set = true; return 0;
+    case GRM_OPT_FROZEN_REC: e->fz_rec = (double)v; e->frozen_set = true; return 0;
+    case GRM_OPT_FROZEN_MAXTAU: std::memcpy(&e->fz_maxtau, &v, sizeof(double)); e->frozen_set = true; return 0;
+    case GRM_OPT_WARMUP: e->warmup = v; return 0;
+    default: e->err = "unknown option"; return -1;
+    }
+}
+
+int grm_engine_track(grm_engine *e, const grm_init_photon *batch, size_t n) {
+    if (!e || (!batch && n)) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (n > e->batch_cap) {
+        if (e->d_batch) hipFree(e->d_batch);
+        e->d_batch = nullptr;
+        HIPCHK(e, hipMalloc(&e->d_batch, n * sizeof(grm_init_photon)));
+        e->batch_cap = n;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_batch, batch, n * sizeof(grm_init_photon), hipMemcpyHostToDevice, e->stream));
+    return run_transport(e, e->d_batch, n);
+}
+
+int grm_engine_track_device(grm_engine *e, const grm_init_photon *dev_batch, size_t n) {
+    if (!e || (!dev_batch && n)) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    return run_transport(e, dev_batch, n);
+}
+
+int grm_engine_finish(grm_engine *e, grm_spectrum_cell *spec, uint64_t *n_rec, uint64_t *n_scatt, double *max_tau) {
+    if (!e) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    DevCounters h;
+    if (spec)
+        HIPCHK(e, hipMemcpyAsync(spec, e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS,
+                                 hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (n_rec) *n_rec = h.n_recorded;
+    if (n_scatt) *n_scatt = h.n_scatt;
+    if (max_tau) std::memcpy(max_tau, &h.max_tau_bits, sizeof(double));
+    e->stats.n_steps = h.n_steps;
+    e->stats.n_tracked = h.n_tracked;
+    e->stats.n_children = h.n_children;
+    e->stats.n_overflow = h.n_overflow;
+    e->stats.n_dropped = h.n_dropped;
+    e->stats.n_primaries = h.n_primaries;
+    return 0;
+}
+
+int grm_engine_reset(grm_engine *e) {
+    if (!e) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    const double ms = e->stats.kernel_ms;
+    const uint64_t launches = e->stats.n_launches;
+    std::memset(&e->stats, 0, sizeof(e->stats));
+    e->stats.kernel_ms = ms;
+    e->stats.n_launches = launches;
+    e->history = 0;
+    return reset_counters(e);
+}
+
+int grm_engine_stats(const grm_engine *e, grm_stats *out) {
+    if (!e || !out) return -1;
+    grm_engine *m = const_cast<grm_engine *>(e);
+    if (grm_engine_finish(m, nullptr, nullptr, nullptr, nullptr)) return -1;
+    *out = e->stats;
+    return 0;
+}
+
+void *grm_engine_spectrum_device_ptr(grm_engine *e) { return e ? (void *)e->d_spec : nullptr; }
+
+int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap) {
+    if (!e || !e->d_trace) return -1;
+    hipSetDevice(e->device);
+    unsigned long long cnt = 0;
+    if (hipMemcpy(&cnt, e->d_small + 3, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    const size_t avail = std::min<unsigned long long>(cnt, e->trace_cap);
+    const size_t k = std::min(avail, cap);
+    if (k && out && hipMemcpy(out, e->d_trace, k * sizeof(grm_trace), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return (int64_t)cnt;
+}
+
+int grm_probe(grm_engine *e, int which, const double *in, int in_stride, double *out, int out_stride, size_t n) {
+    if (!e) return -1;
+    hipSetDevice(e->device);
+    return grm_probe_impl(e->P, e->stream, which, in, in_stride, out, out_stride, n, e->err);
+}
+
+size_t grm_sizeof(int which) {
+    switch (which) {
+    case 0: return sizeof(grm_header);
+    case 1: return sizeof(grm_units);
+    case 2: return sizeof(grm_init_photon);
+    case 3: return sizeof(grm_spectrum_cell);
+    case 4: return sizeof(grm_trace);
+    case 5: return sizeof(grm_stats);
+    default: return 0;
+    }
+}
+
+const char *grm_version(void) { return "grmonty_amd 0.1.0 (gfx950)"; }
+
+} /* extern "C" */

@@ -1,0 +1,292 @@
+"""grmonty_amd -- Python binding of the MI355X superphoton transport engine (C-ABI in
+include/grmonty_amd.h, implemented in cuda-grmonty_amd/libgrmonty_amd.so).
+
+The library is loaded from the source tree; if it is missing the import raises (there is no CPU
+fallback: the transport path is the HIP kernel or nothing).
+
+    m = Model.load(dump_path, photon_n=1_000_000)     # HARMModel(photon_n, mass_unit).read_file
+    m.init(threads)                                     # init(): geometry + tables
+    ph = m.emit(seed=123)                               # emitted superphotons (InitPhoton records)
+    e = Engine(m, device=0)                             # cuda_super_photon::alloc_memory
+    e.track(ph)                                         # track_super_photons
+    spec, n_rec, n_scatt, max_tau = e.finish()
+    m.write_spectrum(spec, "spectrum.txt")              # report_spectrum
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libgrmonty_amd.so")
+REPO_DIR = os.path.dirname(PKG_DIR)
+HEADER_PATH = os.path.join(REPO_DIR, "include", "grmonty_amd.h")
+
+DP = C.POINTER(C.c_double)
+VP = C.c_void_p
+
+INIT_PHOTON = np.dtype([("x", "<f8", 4), ("k", "<f8", 4), ("w", "<f8"), ("e", "<f8"), ("l", "<f8"),
+                        ("n_e_0", "<f8"), ("theta_e_0", "<f8"), ("b_0", "<f8"), ("e_0", "<f8"),
+                        ("n_scatt", "<i4"), ("pad_", "<i4")])
+SPEC_FIELDS = ["dn_dle", "de_dle", "nph", "nscatt", "x1i_av", "x2i_sq", "x3f_sq", "tau_abs", "tau_scatt",
+               "ne_0", "theta_e_0", "b_0", "e_0"]
+SPECTRUM_CELL = np.dtype([(f, "<f8") for f in SPEC_FIELDS])
+TRACE = np.dtype([("id", "<u8"), ("parent_id", "<u8"), ("w", "<f8"), ("e", "<f8"), ("x1", "<f8"), ("x2", "<f8"),
+                  ("x3", "<f8"), ("tau_abs", "<f8"), ("tau_scatt", "<f8"), ("n_scatt", "<i4"),
+                  ("n_step", "<i4"), ("end_reason", "<i4"), ("ix2", "<i4"), ("i_e", "<i4"), ("pad_", "<i4")])
+
+OPT_SEED, OPT_BIAS_MODE, OPT_TRACE_CAP, OPT_GRID_BLOCKS, OPT_ID_BASE = 0, 1, 2, 3, 4
+N_TH_BINS, N_E_BINS = 6, 200
+
+
+class Header(C.Structure):
+    _fields_ = [("t", C.c_double), ("n", C.c_int * 2), ("x_start", C.c_double * 4), ("x_stop", C.c_double * 4),
+                ("dx", C.c_double * 4), ("t_final", C.c_double), ("n_step", C.c_int), ("a", C.c_double),
+                ("gamma", C.c_double), ("courant", C.c_double), ("dt_dump", C.c_double), ("dt_log", C.c_double),
+                ("dt_img", C.c_double), ("dt_rdump", C.c_int), ("cnt_dump", C.c_int), ("cnt_img", C.c_int),
+                ("cnt_rdump", C.c_int), ("dt", C.c_double), ("lim", C.c_int), ("failed", C.c_int),
+                ("r_in", C.c_double), ("r_out", C.c_double), ("h_slope", C.c_double), ("r_0", C.c_double)]
+
+
+class Units(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("mass_unit", "l_unit", "t_unit", "rho_unit", "u_unit", "b_unit",
+                                          "theta_e_unit", "n_e_unit")]
+
+
+class Stats(C.Structure):
+    _fields_ = [("n_tracked", C.c_uint64), ("n_primaries", C.c_uint64), ("n_children", C.c_uint64),
+                ("n_steps", C.c_uint64), ("n_overflow", C.c_uint64), ("n_dropped", C.c_uint64),
+                ("n_launches", C.c_uint64), ("kernel_ms", C.c_double), ("last_kernel_ms", C.c_double),
+                ("last_steps", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every entry point of include/grmonty_amd.h with its ctypes signature
+SIGNATURES = {
+    "grm_engine_create": (C.c_int, [C.POINTER(Header), C.POINTER(DP), C.POINTER(Units), DP, DP, DP, C.c_int,
+                                    C.POINTER(VP)]),
+    "grm_engine_destroy": (None, [VP]),
+    "grm_engine_last_error": (C.c_char_p, [VP]),
+    "grm_engine_set_option": (C.c_int, [VP, C.c_int, C.c_int64]),
+    "grm_engine_track": (C.c_int, [VP, VP, C.c_size_t]),
+    "grm_engine_track_device": (C.c_int, [VP, VP, C.c_size_t]),
+    "grm_engine_finish": (C.c_int, [VP, VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), DP]),
+    "grm_engine_reset": (C.c_int, [VP]),
+    "grm_engine_stats": (C.c_int, [VP, C.POINTER(Stats)]),
+    "grm_engine_spectrum_device_ptr": (VP, [VP]),
+    "grm_engine_trace": (C.c_int64, [VP, VP, C.c_size_t]),
+    "grm_model_load": (C.c_int, [C.c_char_p, C.c_int, C.c_double, C.POINTER(VP)]),
+    "grm_model_free": (None, [VP]),
+    "grm_model_last_error": (C.c_char_p, []),
+    "grm_model_init": (C.c_int, [VP, C.c_int]),
+    "grm_model_header": (None, [VP, C.POINTER(Header)]),
+    "grm_model_units": (None, [VP, C.POINTER(Units)]),
+    "grm_model_scalars": (None, [VP, DP]),
+    "grm_model_field": (DP, [VP, C.c_int]),
+    "grm_model_table": (DP, [VP, C.c_int]),
+    "grm_engine_create_from_model": (C.c_int, [VP, C.c_int, C.POINTER(VP)]),
+    "grm_model_emit": (C.c_int64, [VP, C.c_uint64, C.c_int64, C.c_int64, VP, C.c_size_t, C.c_int]),
+    "grm_model_zone_weights": (C.c_int, [VP, DP]),
+    "grm_write_spectrum": (C.c_int, [VP, VP, C.c_char_p, DP]),
+    "grm_probe": (C.c_int, [VP, C.c_int, DP, C.c_int, DP, C.c_int, C.c_size_t]),
+    "grm_sizeof": (C.c_size_t, [C.c_int]),
+    "grm_version": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree C-ABI library; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C cuda-grmonty_amd` or __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Model:
+    """HARMModel host side (loader, tables, emission, writer) -- C++ in libgrmonty_amd.so."""
+
+    TABLE_SIZES = {0: 221 * 81, 1: 201, 2: 201, 3: 201, 4: 20001, 5: 20001}
+
+    def __init__(self, handle):
+        self.L = lib()
+        self.h = handle
+
+    @classmethod
+    def load(cls, path: str, photon_n: int = 5_000_000, mass_unit: float = 4e19) -> "Model":
+        L = lib()
+        h = VP()
+        if L.grm_model_load(path.encode(), int(photon_n), float(mass_unit), C.byref(h)) != 0:
+            raise IOError(L.grm_model_last_error().decode())
+        return cls(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.grm_model_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def init(self, n_threads: int = 0) -> "Model":
+        if self.L.grm_model_init(self.h, int(n_threads)) != 0:
+            raise RuntimeError(self.L.grm_model_last_error().decode())
+        return self
+
+    @property
+    def header(self) -> Header:
+        h = Header()
+        self.L.grm_model_header(self.h, C.byref(h))
+        return h
+
+    @property
+    def units(self) -> Units:
+        u = Units()
+        self.L.grm_model_units(self.h, C.byref(u))
+        return u
+
+    def scalars(self) -> dict:
+        o = np.zeros(5)
+        self.L.grm_model_scalars(self.h, o.ctypes.data_as(DP))
+        return dict(bias_norm=o[0], x1_min=o[1], max_tau_scatt=o[2], d_tau_k=o[3], rh=o[4])
+
+    def field(self, which: int) -> np.ndarray:
+        h = self.header
+        n = h.n[0] * h.n[1]
+        return np.ctypeslib.as_array(self.L.grm_model_field(self.h, which), shape=(n,)).copy().reshape(h.n[0], h.n[1])
+
+    def table(self, which: int) -> np.ndarray:
+        if which == 6:
+            h = self.header
+            n = h.n[0] * h.n[1]
+        else:
+            n = self.TABLE_SIZES[which]
+        return np.ctypeslib.as_array(self.L.grm_model_table(self.h, which), shape=(n,)).copy()
+
+    def count(self, seed: int = 123, z0: int = 0, z1: int = -1, threads: int = 0) -> int:
+        n = self.L.grm_model_emit(self.h, seed, z0, z1, None, 0, threads)
+        if n < 0:
+            raise RuntimeError(self.L.grm_model_last_error().decode())
+        return int(n)
+
+    def emit(self, seed: int = 123, z0: int = 0, z1: int = -1, threads: int = 0) -> np.ndarray:
+        n = self.count(seed, z0, z1, threads)
+        out = np.zeros(n, dtype=INIT_PHOTON)
+        got = self.L.grm_model_emit(self.h, seed, z0, z1, _ptr(out), n, threads)
+        if got != n:
+            raise RuntimeError(self.L.grm_model_last_error().decode())
+        return out
+
+    def zone_weights(self) -> np.ndarray:
+        h = self.header
+        out = np.zeros(h.n[0] * h.n[1])
+        if self.L.grm_model_zone_weights(self.h, out.ctypes.data_as(DP)) != 0:
+            raise RuntimeError(self.L.grm_model_last_error().decode())
+        return out
+
+    def write_spectrum(self, spectrum: np.ndarray, path: str | None):
+        s = np.ascontiguousarray(spectrum, dtype=SPECTRUM_CELL).reshape(-1)
+        o = np.zeros(2)
+        if self.L.grm_write_spectrum(self.h, _ptr(s), path.encode() if path else None, o.ctypes.data_as(DP)) != 0:
+            raise IOError(self.L.grm_model_last_error().decode())
+        return dict(luminosity=o[0], max_tau_scatt=o[1])
+
+
+class Engine:
+    """cuda_super_photon replacement: device buffers + persistent transport kernel on one GPU."""
+
+    def __init__(self, model: Model, device: int = 0):
+        self.L = lib()
+        h = VP()
+        rc = self.L.grm_engine_create_from_model(model.h, int(device), C.byref(h))
+        if rc != 0:
+            msg = self.L.grm_engine_last_error(h).decode() if h else self.L.grm_model_last_error().decode()
+            if h:
+                self.L.grm_engine_destroy(h)
+            raise RuntimeError(f"engine creation failed: {msg}")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.grm_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(self.L.grm_engine_last_error(self.h).decode())
+
+    def set_option(self, opt: int, value: int):
+        self._check(self.L.grm_engine_set_option(self.h, opt, int(value)))
+
+    def track(self, photons: np.ndarray):
+        ph = np.ascontiguousarray(photons, dtype=INIT_PHOTON)
+        self._check(self.L.grm_engine_track(self.h, _ptr(ph), len(ph)))
+
+    def track_device(self, dev_ptr: int, n: int):
+        self._check(self.L.grm_engine_track_device(self.h, C.c_void_p(dev_ptr), int(n)))
+
+    def finish(self):
+        spec = np.zeros(N_TH_BINS * N_E_BINS, dtype=SPECTRUM_CELL)
+        nr, ns, mt = C.c_uint64(), C.c_uint64(), C.c_double()
+        self._check(self.L.grm_engine_finish(self.h, _ptr(spec), C.byref(nr), C.byref(ns), C.byref(mt)))
+        return spec.reshape(N_TH_BINS, N_E_BINS), nr.value, ns.value, mt.value
+
+    def reset(self):
+        self._check(self.L.grm_engine_reset(self.h))
+
+    def stats(self) -> dict:
+        s = Stats()
+        self._check(self.L.grm_engine_stats(self.h, C.byref(s)))
+        return s.as_dict()
+
+    def spectrum_device_ptr(self) -> int:
+        return int(self.L.grm_engine_spectrum_device_ptr(self.h))
+
+    def trace(self, cap: int) -> np.ndarray:
+        out = np.zeros(max(cap, 1), dtype=TRACE)
+        n = self.L.grm_engine_trace(self.h, _ptr(out), cap)
+        if n < 0:
+            raise RuntimeError("trace not enabled")
+        return out[:min(n, cap)]
+
+    def probe(self, which: int, inputs: np.ndarray, out_width: int) -> np.ndarray:
+        a = np.ascontiguousarray(inputs, dtype=np.float64)
+        if a.ndim == 1:
+            a = a[:, None]
+        out = np.zeros((a.shape[0], out_width))
+        self._check(self.L.grm_probe(self.h, which, a.ctypes.data_as(DP), a.shape[1], out.ctypes.data_as(DP),
+                                     out_width, a.shape[0]))
+        return out
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Names of the functions declared in the public C header (for the ABI test)."""
+    import re
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(grm_[a-z0-9_]+)\s*\(", txt)))

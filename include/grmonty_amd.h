@@ -1,0 +1,208 @@
+/*
+ * grmonty_amd.h -- C-ABI of the MI355X-native grmonty superphoton transport engine.
+ *
+ * Drop-in boundary for the reference's device boundary, namespace
+ * cuda_super_photon (reference: cuda_grmonty/super_photon.cuh:15-63), plus the
+ * host model API that HARMModel's callers use (harm_model.hpp / main.cpp).
+ * Plain C: POD structs, pointers and sizes; no torch, no C++ types; every entry
+ * point returns an int status (0 = OK) and never exits or throws across the ABI.
+ *
+ *   reference (CUDA build)                                 this ABI
+ *   ------------------------------------------------------------------------------------
+ *   cuda_super_photon::alloc_memory(header, data, units,   grm_engine_create()
+ *       hotcross, f, k2)          super_photon.cuh:29-34
+ *   cuda_super_photon::track_super_photons(bias_norm,      grm_engine_track() /
+ *       max_tau_scatt, photon_queue, done_sem, spectrum,     grm_engine_track_device()
+ *       n_rec, n_scatt)           super_photon.cuh:55-61     + grm_engine_finish()
+ *   cuda_super_photon::free_memory()  super_photon.cuh:40    grm_engine_destroy()
+ *   gpuErrchk -> exit()           utils.cuh:20-40          int status + grm_engine_last_error()
+ *
+ * The reference hands photons over through a C++ ConcurrentQueue + binary
+ * semaphore (not expressible in C); here the host hands over batches of
+ * InitPhoton records (photon.hpp:41-52) and scattered children stay on the
+ * device (per-lane stacks + an overflow pool), never round-tripping over PCIe.
+ */
+#ifndef GRMONTY_AMD_H
+#define GRMONTY_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GRM_N_TH_BINS 6
+#define GRM_N_E_BINS 200
+#define GRM_N_E_SAMP 200
+#define GRM_HC_N_W 220
+#define GRM_HC_N_T 80
+#define GRM_NINT 20000
+
+/* harm_data.hpp:19-44 -- HARM dump header (same field order/types as the reference) */
+typedef struct grm_header {
+    double t;
+    int n[2];
+    double x_start[4];
+    double x_stop[4];
+    double dx[4];
+    double t_final;
+    int n_step;
+    double a;
+    double gamma;
+    double courant;
+    double dt_dump;
+    double dt_log;
+    double dt_img;
+    int dt_rdump;
+    int cnt_dump;
+    int cnt_img;
+    int cnt_rdump;
+    double dt;
+    int lim;
+    int failed;
+    double r_in;
+    double r_out;
+    double h_slope;
+    double r_0;
+} grm_header;
+
+/* harm_data.hpp:62-71 */
+typedef struct grm_units {
+    double mass_unit, l_unit, t_unit, rho_unit, u_unit, b_unit, theta_e_unit, n_e_unit;
+} grm_units;
+
+/* photon.hpp:41-52 -- emitted superphoton (15 doubles + int), 128 B */
+typedef struct grm_init_photon {
+    double x[4];
+    double k[4];
+    double w, e, l, n_e_0, theta_e_0, b_0, e_0;
+    int n_scatt;
+    int pad_;
+} grm_init_photon;
+
+/* harm_data.hpp:129-143 -- one (theta, energy) spectrum cell, reference field order */
+typedef struct grm_spectrum_cell {
+    double dn_dle, de_dle, nph, nscatt, x1i_av, x2i_sq, x3f_sq, tau_abs, tau_scatt, ne_0, theta_e_0, b_0, e_0;
+} grm_spectrum_cell;
+
+/* end-of-life record of one tracked superphoton (debug / parity traces) */
+typedef struct grm_trace {
+    uint64_t id;
+    uint64_t parent_id;
+    double w, e, x1, x2, x3, tau_abs, tau_scatt;
+    int32_t n_scatt;
+    int32_t n_step;
+    int32_t end_reason; /* 0 recorded, 1 escaped-unbinned, 2 absorbed/horizon/roulette, 3 max-step, 4 invalid */
+    int32_t ix2;
+    int32_t i_e;
+    int32_t pad_;
+} grm_trace;
+
+typedef struct grm_stats {
+    uint64_t n_tracked;        /* superphotons tracked (primaries + scattered children) */
+    uint64_t n_primaries;      /* emitted photons consumed (the reference's "created") */
+    uint64_t n_children;       /* scattered children spawned on device */
+    uint64_t n_steps;          /* transport loop iterations (geodesic pushes), reference n_step unit */
+    uint64_t n_overflow;       /* children that spilled from lane stacks to the overflow pool */
+    uint64_t n_dropped;        /* children lost to a full overflow pool (must be 0) */
+    uint64_t n_launches;       /* transport kernel launches */
+    double kernel_ms;          /* summed transport-kernel time (HIP events on the engine stream) */
+    double last_kernel_ms;     /* duration of the most recent transport call's kernels */
+    uint64_t last_steps;       /* steps in the most recent transport call */
+} grm_stats;
+
+typedef struct grm_engine grm_engine;
+
+/* Engine options (grm_engine_set_option) */
+enum {
+    GRM_OPT_SEED = 0,        /* Philox key for transport RNG streams (default 123, consts.hpp:14) */
+    GRM_OPT_BIAS_MODE = 1,   /* 0 live device counters (default, reference-like adaptive bias), 1 frozen */
+    GRM_OPT_TRACE_CAP = 2,   /* >0 enables per-photon trace buffer with this capacity */
+    GRM_OPT_GRID_BLOCKS = 3, /* persistent grid size override (0 = auto) */
+    GRM_OPT_ID_BASE = 4,     /* first photon stream id of the next track call */
+    /* frozen-bias snapshot (used when GRM_OPT_BIAS_MODE = 1; default: counters at call start) */
+    GRM_OPT_FROZEN_SCATT = 5,  /* N_scatt */
+    GRM_OPT_FROZEN_REC = 6,    /* N_recorded */
+    GRM_OPT_FROZEN_MAXTAU = 7, /* max tau_scatt, IEEE-754 bit pattern of the double */
+    /* live-bias warm-up: until this many photons have been tracked since the last reset, a
+     * batch is cut into launches that double the history each time, so the adaptive bias
+     * counters evolve as in the serial reference (-1 = one persistent grid's worth of lanes, 0 = off) */
+    GRM_OPT_WARMUP = 8
+};
+
+/* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
+/* fields: 8 row-major [n1][n2] arrays (x2 fastest): rho, u, u1, u2, u3, B1, B2, B3.
+ * hotcross: (GRM_HC_N_W+1)*(GRM_HC_N_T+1) log10 sigma table; k2: GRM_N_E_SAMP+1 log K2 table.
+ * scalars: bias_norm, x1_min (= log r_h), max_tau_scatt (initial), d_tau_k. */
+int grm_engine_create(const grm_header *header, const double *const fields[8], const grm_units *units,
+                      const double *hotcross, const double *k2, const double scalars[4], int device,
+                      grm_engine **out);
+void grm_engine_destroy(grm_engine *e);
+const char *grm_engine_last_error(const grm_engine *e);
+int grm_engine_set_option(grm_engine *e, int opt, int64_t value);
+
+/* --- transport (super_photon.cuh:55-61) ------------------------------------------------- */
+/* host batch -> device copy -> persistent transport; synchronous. */
+int grm_engine_track(grm_engine *e, const grm_init_photon *batch, size_t n);
+/* batch already resident in device memory (e.g. a torch tensor's data_ptr); synchronous. */
+int grm_engine_track_device(grm_engine *e, const grm_init_photon *dev_batch, size_t n);
+/* copy out accumulated spectrum [GRM_N_TH_BINS][GRM_N_E_BINS] and counters (does not reset). */
+int grm_engine_finish(grm_engine *e, grm_spectrum_cell *spectrum_out, uint64_t *n_recorded, uint64_t *n_scatt,
+                      double *max_tau_scatt);
+/* zero the spectrum and counters; max_tau_scatt back to its initial value. */
+int grm_engine_reset(grm_engine *e);
+int grm_engine_stats(const grm_engine *e, grm_stats *out);
+/* device pointer of the spectrum accumulator (GRM_N_TH_BINS*GRM_N_E_BINS cells), for in-place
+ * collectives (RCCL all-reduce over xGMI) without a host round trip. */
+void *grm_engine_spectrum_device_ptr(grm_engine *e);
+/* copy the per-photon trace (requires GRM_OPT_TRACE_CAP > 0); returns records produced. */
+int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap);
+
+/* --- host model (harm_model.hpp; C++ host, no GPU) ------------------------------------- */
+typedef struct grm_model grm_model;
+/* HARMModel(photon_n, mass_unit) + read_file(path)   harm_model.cpp:64-232 */
+int grm_model_load(const char *path, int photon_n, double mass_unit, grm_model **out);
+void grm_model_free(grm_model *m);
+const char *grm_model_last_error(void);
+/* init(): geometry, hotcross, emission tables, weight, nint    harm_model.cpp:234-240 */
+int grm_model_init(grm_model *m, int n_threads);
+void grm_model_header(const grm_model *m, grm_header *h);
+void grm_model_units(const grm_model *m, grm_units *u);
+/* bias_norm, x1_min, max_tau_scatt (initial), d_tau_k, rh */
+void grm_model_scalars(const grm_model *m, double out[5]);
+/* 0 rho 1 u 2 u1 3 u2 4 u3 5 B1 6 B2 7 B3 */
+const double *grm_model_field(const grm_model *m, int which);
+/* 0 hotcross 1 k2 2 f 3 weight 4 nint 5 dndlnu_max 6 det */
+const double *grm_model_table(const grm_model *m, int which);
+/* create an engine from a loaded + initialised model */
+int grm_engine_create_from_model(const grm_model *m, int device, grm_engine **out);
+
+/* Emission (harm_model.cpp:673-892): zone-parallel, deterministic for a given seed whatever
+ * n_threads is (per-zone Philox streams).  Returns photons written (<= cap) or -1 on error.
+ * Call with out=NULL to only count (exact).  zone range [z0, z1) in row-major zone order
+ * (z1 < 0 = all) -- used to shard emission across ranks. */
+int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon *out, size_t cap,
+                       int n_threads);
+/* cumulative expected photon count per zone, for balanced zone-range sharding (n1*n2 doubles) */
+int grm_model_zone_weights(const grm_model *m, double *out);
+
+/* report_spectrum (harm_model.cpp:416-471): 200 rows x 37 columns "%10.5g ".
+ * out2 (optional): luminosity, max tau_scatt. */
+int grm_write_spectrum(const grm_model *m, const grm_spectrum_cell *spectrum, const char *path, double out2[2]);
+
+/* --- per-function device probes (parity tests; one lane per input) --------------------- */
+/* which: see GRM_PROBE_* in DESIGN.md / csrc/grm_probe.hip. in/out are host arrays of
+ * n * in_stride / n * out_stride doubles. */
+int grm_probe(grm_engine *e, int which, const double *in, int in_stride, double *out, int out_stride, size_t n);
+
+/* ABI introspection: sizes of the POD structs (0 header 1 units 2 init_photon 3 spectrum_cell
+ * 4 trace 5 stats) */
+size_t grm_sizeof(int which);
+const char *grm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GRMONTY_AMD_H */

@@ -1,0 +1,1994 @@
+/*
+ * grmonty_oracle.cpp -- CPU ORACLE: clean-room restatement of the reference's
+ * CPU transport path (m-torhan/cuda-grmonty @ /root/reference).
+ *
+ * TEST INFRASTRUCTURE ONLY.  The product (HIP kernels + C++ host under
+ * cuda-grmonty_amd/) never links, loads or calls anything in oracle/.
+ *
+ * Every function cites the reference file:line it restates.  Arithmetic is
+ * written in the reference's evaluation order (left-to-right products,
+ * same constant folding) so that, compiled with g++ -O2 (no FMA contraction on
+ * x86-64), results are bit-identical to the reference CPU build wherever the
+ * same libm / libstdc++ calls are made.  Pure calls hoisted out of loops
+ * (hotcross dnd_gamma_e, whose value depends only on (theta_e, gamma_e)) give
+ * identical bits.
+ *
+ * RNG: GRMO_RNG_MT19937 reproduces monty_rand.cpp:19-31 (std::mt19937,
+ * std::uniform_real_distribution<double>, std::chi_squared_distribution).
+ * GRMO_RNG_PHILOX is the device stream definition (Philox4x32-10 per photon id),
+ * used to compare the HIP path photon-by-photon.
+ */
+#include "grmonty_oracle.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <stdexcept>
+#include <queue>
+#include <random>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+namespace grmo {
+
+/* ------------------------------------------------------------------------- */
+/* constants: consts.hpp:14-157                                              */
+/* ------------------------------------------------------------------------- */
+constexpr double kPi = 3.141592653589793238462643383279502884; /* std::numbers::pi */
+constexpr double kSqrt2 = 1.414213562373095048801688724209698079;
+constexpr double kLn10 = 2.302585092994045684017991454684364208;
+constexpr double EPS = 1.0e-40;
+constexpr int N_E_SAMP = 200, N_E_BINS = 200, N_TH_BINS = 6;
+constexpr double NU_MIN = 1.0e9, NU_MAX = 1.0e16;
+constexpr double THETA_E_MIN = 0.3, TP_OVER_TE = 3.0;
+constexpr double WEIGHT_MIN = 1.0e31, ROULETTE = 1.0e4;
+constexpr double R_MAX = 100.0;
+constexpr double STEP_EPS = 0.04, E_TOL = 1.0e-3;
+constexpr int MAX_ITER = 2, MAX_N_STEP = 1280000;
+constexpr double EE = 4.80320680e-10, CL = 2.99792458e10, ME = 9.1093826e-28, MP = 1.67262171e-24;
+constexpr double HPL = 6.6260693e-27, HBAR = HPL / (2. * kPi), KBOL = 1.3806505e-16, G_NEWT = 6.6742e-8;
+constexpr double SIGMA_THOMSON = 0.665245873e-24;
+constexpr double M_SUN = 1.989e33, L_SUN = 3.827e33, M_BH = 4.0e6 * M_SUN;
+constexpr int NINT = 20000;
+constexpr double BTHSQ_MIN = 1.0e-4, BTHSQ_MAX = 1.0e8;
+/* hotcross grid consts.hpp:97-110 */
+constexpr double HC_MIN_W = 1.0e-12, HC_MAX_W = 1.0e6, HC_MIN_T = 1.0e-4, HC_MAX_T = 1.0e4;
+constexpr int HC_N_W = 220, HC_N_T = 80;
+constexpr double HC_MAX_GAMMA = 12.0, HC_D_MU_E = 0.05, HC_D_GAMMA_E = 0.05;
+/* jnu consts.hpp:122-137 */
+constexpr double JNU_MIN_K = 0.002, JNU_MAX_K = 1.0e7, JNU_MIN_T = THETA_E_MIN, JNU_MAX_T = 1.0e2;
+constexpr double JNU_CST = 1.88774862536;
+constexpr double JNU_K_FAC = 9 * kPi * ME * CL / EE;
+constexpr double JCST = kSqrt2 * EE * EE * EE / (27.0 * ME * CL * CL); /* consts.hpp:146 */
+constexpr double SPEC_D_L_E = 0.25;
+
+struct Derived {
+    double l_nu_min, l_nu_max, n_l_n, d_l_nu, x1_max, l_b_min, d_l_b;
+    double hc_l_min_w, hc_l_min_t, hc_d_l_w, hc_d_l_t;
+    double jnu_l_min_k, jnu_d_l_k, jnu_l_min_t, jnu_d_l_t;
+    double spec_l_e_0;
+    Derived() {
+        l_nu_min = std::log(NU_MIN);
+        l_nu_max = std::log(NU_MAX);
+        n_l_n = l_nu_max - l_nu_min;
+        d_l_nu = (l_nu_max - l_nu_min) / N_E_SAMP;
+        x1_max = std::log(R_MAX);
+        l_b_min = std::log(BTHSQ_MIN);
+        d_l_b = std::log(BTHSQ_MAX / BTHSQ_MIN) / NINT;
+        hc_l_min_w = std::log10(HC_MIN_W);
+        hc_l_min_t = std::log10(HC_MIN_T);
+        hc_d_l_w = std::log10(HC_MAX_W / HC_MIN_W) / HC_N_W;
+        hc_d_l_t = std::log10(HC_MAX_T / HC_MIN_T) / HC_N_T;
+        jnu_l_min_k = std::log(JNU_MIN_K);
+        jnu_d_l_k = std::log(JNU_MAX_K / JNU_MIN_K) / N_E_SAMP;
+        jnu_l_min_t = std::log(JNU_MIN_T);
+        jnu_d_l_t = std::log(JNU_MAX_T / JNU_MIN_T) / N_E_SAMP;
+        spec_l_e_0 = std::log(1.0e-12);
+    }
+};
+static const Derived D;
+
+typedef grmo_header Header;
+typedef grmo_units Units;
+typedef grmo_fluid Fluid;
+
+/* photon.hpp:19-36 */
+struct Photon {
+    double x[4], k[4], dkdlam[4];
+    double w, e, l, x1i, x2i, tau_abs, tau_scatt, n_e_0, theta_e_0, b_0, e_0, e_0_s;
+    int n_scatt;
+    uint64_t id, parent_id;
+};
+
+/* ------------------------------------------------------------------------- */
+/* RNG                                                                        */
+/* ------------------------------------------------------------------------- */
+static inline void philox_round(uint32_t c[4], const uint32_t k[2]) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    const uint32_t n0 = hi1 ^ c[1] ^ k[0];
+    const uint32_t n2 = hi0 ^ c[3] ^ k[1];
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+}
+
+static inline void philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    uint32_t k[2] = {key[0], key[1]};
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k[0] += 0x9E3779B9u;
+            k[1] += 0xBB67AE85u;
+        }
+        philox_round(c, k);
+    }
+    for (int i = 0; i < 4; ++i) out[i] = c[i];
+}
+
+static inline uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* child stream id: deterministic function of the parent's stream position */
+static inline uint64_t child_id(uint64_t parent_id, uint64_t parent_ctr) {
+    return splitmix64(parent_id ^ (0x9E3779B97F4A7C15ull * (parent_ctr + 1)));
+}
+
+struct Rng {
+    int mode = GRMO_RNG_MT19937;
+    std::mt19937 *mt = nullptr; /* shared stream (reference semantics) */
+    std::mt19937 own;
+    uint32_t key[2] = {0, 0};
+    uint64_t id = 0, ctr = 0;
+
+    double uniform() {
+        if (mode == GRMO_RNG_MT19937) {
+            std::uniform_real_distribution<double> dist(0, 1); /* monty_rand.cpp:23-26 */
+            return dist(*mt);
+        }
+        uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)id, (uint32_t)(id >> 32)};
+        uint32_t o[4];
+        philox4x32_10(c, key, o);
+        ++ctr;
+        const uint64_t m = ((((uint64_t)o[1]) << 32) | o[0]) >> 11; /* 53 bits */
+        return (double)(m + 1) * (1.0 / 9007199254740992.0);       /* (0, 1] */
+    }
+    double chi_sq(int dof) {
+        if (mode == GRMO_RNG_MT19937) {
+            std::chi_squared_distribution<double> chi(dof); /* monty_rand.cpp:28-31 */
+            return chi(*mt);
+        }
+        /* device definition: chi2(2m) = -2 ln(u1..um), odd dof adds one Box-Muller normal^2 */
+        double prod = uniform();
+        const int m = dof / 2;
+        for (int i = 1; i < m; ++i) prod *= uniform();
+        double x = -2.0 * std::log(prod);
+        if (dof & 1) {
+            const double ua = uniform();
+            const double ub = uniform();
+            const double z = std::sqrt(-2.0 * std::log(ua)) * std::cos(2.0 * kPi * ub);
+            x += z * z;
+        }
+        return x;
+    }
+    static Rng philox(uint64_t seed, uint64_t id) {
+        Rng r;
+        r.mode = GRMO_RNG_PHILOX;
+        r.key[0] = (uint32_t)seed;
+        r.key[1] = (uint32_t)(seed >> 32);
+        r.id = id;
+        r.ctr = 0;
+        return r;
+    }
+};
+
+/* ------------------------------------------------------------------------- */
+/* GK61: integration.cpp:144-236 (adaptive bisection on a max-error heap)     */
+/* Kronrod 61-point nodes/weights and Gauss 30-point weights (QUADPACK qk61). */
+/* ------------------------------------------------------------------------- */
+static const double XGK[31] = {
+    0.999484410050490637571325895705811, 0.996893484074649540271630050918695, 0.991630996870404594858628366109486,
+    0.983668123279747209970032581605663, 0.973116322501126268374693868423707, 0.960021864968307512216871025581798,
+    0.944374444748559979415831324037439, 0.926200047429274325879324277080474, 0.905573307699907798546522558925958,
+    0.882560535792052681543116462530226, 0.857205233546061098958658510658944, 0.829565762382768397442898119732502,
+    0.799727835821839083013668942322683, 0.767777432104826194917977340974503, 0.733790062453226804726171131369528,
+    0.697850494793315796932292388026640, 0.660061064126626961370053668149271, 0.620526182989242861140477556431189,
+    0.579345235826361691756024932172540, 0.536624148142019899264169793311073, 0.492480467861778574993693061207709,
+    0.447033769538089176780609900322854, 0.400401254830394392535476211542661, 0.352704725530878113471037207089374,
+    0.304073202273625077372677107199257, 0.254636926167889846439805129817805, 0.204525116682309891438957671002025,
+    0.153869913608583546963794672743256, 0.102806937966737030147096751318001, 0.051471842555317695833025213166723,
+    0.0};
+static const double WGK[31] = {
+    0.001389013698677007624551591226760, 0.003890461127099884051267201844516, 0.006630703915931292173319826369750,
+    0.009273279659517763428441146892024, 0.011823015253496341742232898853251, 0.014369729507045804812451432443580,
+    0.016920889189053272627572289420322, 0.019414141193942381173408951050128, 0.021828035821609192297167485738339,
+    0.024191162078080601365686370725232, 0.026509954882333101610601709335075, 0.028754048765041292843978785354334,
+    0.030907257562387762472884252943092, 0.032981447057483726031814191016854, 0.034979338028060024137499670731468,
+    0.036882364651821229223911065617136, 0.038678945624727592950348651532281, 0.040374538951535959111995279752468,
+    0.041969810215164246147147541285970, 0.043452539701356069316831728117073, 0.044814800133162663192355551616723,
+    0.046059238271006988116271735559374, 0.047185546569299153945261478181099, 0.048185861757087129140779492298305,
+    0.049055434555029778887528165367238, 0.049795683427074206357811569379942, 0.050405921402782346840893085653585,
+    0.050881795898749606492297473049805, 0.051221547849258772170656282604944, 0.051426128537459025933862879215781,
+    0.051494729429451567558340433647099};
+static const double WG[15] = {
+    0.007968192496166605615465883474674, 0.018466468311090959142302131912047, 0.028784707883323369349719179611292,
+    0.038799192569627049596801936446348, 0.048402672830594052902938140422808, 0.057493156217619066481721689402056,
+    0.065974229882180495128128515115962, 0.073755974737705206268243850022191, 0.080755895229420215354694938460530,
+    0.086899787201082979802387530715126, 0.092122522237786128717632707087619, 0.096368737174644259639468626351810,
+    0.099593420586795267062780282103569, 0.101762389748405504596428952168554, 0.102852652893558840341285636705415};
+
+/* integration.cpp:184-236 */
+static void qk61(const std::function<double(double)> &f, double a, double b, double &res, double &err_out) {
+    const double eps = std::numeric_limits<double>::epsilon();
+    const double c = 0.5 * (a + b), h = 0.5 * (b - a);
+    const double fc = f(c);
+    double rk = fc * WGK[30], rg = 0.0, rabs = std::abs(fc) * WGK[30], rasc = 0.0;
+    double f1s[30], f2s[30];
+    for (int i = 0; i < 30; ++i) {
+        const double absc = h * XGK[i];
+        const double f1 = f(c - absc), f2 = f(c + absc);
+        f1s[i] = f1;
+        f2s[i] = f2;
+        const double fs = f1 + f2;
+        rk += WGK[i] * fs;
+        rabs += WGK[i] * (std::abs(f1) + std::abs(f2));
+        if (i % 2 == 1) rg += WG[i / 2] * fs;
+    }
+    rk *= h;
+    rg *= h;
+    rabs *= h;
+    const double mean = rk / (b - a);
+    rasc += WGK[30] * std::abs(fc - mean);
+    for (int i = 0; i < 30; ++i) rasc += WGK[i] * (std::abs(f1s[i] - mean) + std::abs(f2s[i] - mean));
+    rasc *= h;
+    double err = std::abs(rk - rg);
+    if (rasc != 0.0 && err != 0.0) {
+        const double s = std::pow(200.0 * err / rasc, 1.5);
+        err = (s < 1.0) ? rasc * s : rasc;
+    }
+    if (rasc == 0.0 || err < 50 * eps * rabs) err = 0.0;
+    res = rk;
+    err_out = err;
+}
+
+struct Iv {
+    double a, b, r, e;
+    bool operator<(const Iv &o) const { return e < o.e; }
+};
+
+/* integration.cpp:144-181 */
+static double gk61(const std::function<double(double)> &f, double a, double b, double eps_abs, double eps_rel,
+                   int max_iv) {
+    std::priority_queue<Iv> q;
+    double r0, e0;
+    qk61(f, a, b, r0, e0);
+    q.push({a, b, r0, e0});
+    double tot = r0, tot_err = e0;
+    int used = 1;
+    while (!q.empty()) {
+        if (tot_err <= std::max(eps_abs, eps_rel * std::abs(tot))) break;
+        if (used >= max_iv) throw std::runtime_error("Failed to converge within max_intervals.");
+        Iv cur = q.top();
+        q.pop();
+        const double mid = 0.5 * (cur.a + cur.b);
+        double r1, e1, r2, e2;
+        qk61(f, cur.a, mid, r1, e1);
+        qk61(f, mid, cur.b, r2, e2);
+        tot += (r1 + r2 - cur.r);
+        tot_err += (e1 + e2 - cur.e);
+        q.push({cur.a, mid, r1, e1});
+        q.push({mid, cur.b, r2, e2});
+        used += 1;
+    }
+    return tot;
+}
+
+/* ------------------------------------------------------------------------- */
+/* hotcross: hotcross.cpp:60-181                                              */
+/* ------------------------------------------------------------------------- */
+static double hc_klein_nishina(double w) { /* hotcross.cpp:144-151 */
+    if (w < 1.0e-3) return (1.0 - 2.0 * w);
+    return (3.0 / 4.0) * (2.0 / (w * w) + (1.0 / (2.0 * w) - (1.0 + w) / (w * w * w)) * std::log(1.0 + 2.0 * w) +
+                          (1.0 + w) / ((1.0 + 2.0 * w) * (1.0 + 2.0 * w)));
+}
+
+static double dnd_k2f(double theta_e) { /* hotcross.cpp:156-160 (theta-only part of dnd_gamma_e) */
+    if (theta_e > 1.0e-2) return std::cyl_bessel_k(2, 1.0 / theta_e) * std::exp(1.0 / theta_e);
+    return std::sqrt(kPi * theta_e / 2.0);
+}
+
+static double dnd_gamma_e_k(double theta_e, double gamma_e, double k2f) { /* hotcross.cpp:162 */
+    return ((gamma_e * std::sqrt(gamma_e * gamma_e - 1.) / (theta_e * k2f)) * std::exp(-(gamma_e - 1.) / theta_e));
+}
+
+/* hotcross.cpp:108-142; the dnd_gamma_e factor depends only on (theta_e, gamma_e) and is hoisted (same bits) */
+double hotcross_num(double w, double theta_e) {
+    if (std::isnan(w)) return 0.0;
+    if (theta_e < HC_MIN_T && w < HC_MIN_W) return SIGMA_THOMSON;
+    if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
+    const double k2f = dnd_k2f(theta_e);
+    std::vector<double> gam, fv, vv;
+    for (double g = 1.0 + 0.5 * theta_e * HC_D_GAMMA_E; g < 1.0 + HC_MAX_GAMMA * theta_e; g += theta_e * HC_D_GAMMA_E) {
+        gam.push_back(g);
+        fv.push_back(0.5 * dnd_gamma_e_k(theta_e, g, k2f));
+        vv.push_back(std::sqrt(g * g - 1.0) / g);
+    }
+    double cross = 0.0;
+    for (double mu_e = -1.0 + 0.5 * HC_D_MU_E; mu_e < 1.0; mu_e += HC_D_MU_E) {
+        for (size_t t = 0; t < gam.size(); ++t) {
+            const double v = vv[t];
+            const double we = w * gam[t] * (1.0 - mu_e * v); /* boostcross, hotcross.cpp:164-181 */
+            const double bc = hc_klein_nishina(we) * (1.0 - mu_e * v);
+            cross += theta_e * HC_D_MU_E * HC_D_GAMMA_E * bc * fv[t];
+        }
+    }
+    return cross * SIGMA_THOMSON;
+}
+
+/* ------------------------------------------------------------------------- */
+/* jnu_mixed: jnu_mixed.cpp:57-158                                            */
+/* ------------------------------------------------------------------------- */
+static double jnu_integrand(double th, double k) { /* jnu_mixed.cpp:127-137 */
+    const double sin_th = std::sin(th);
+    const double x = k / sin_th;
+    if (sin_th < 1.0e-150 || x > 2.0e8) return 0.0;
+    return sin_th * sin_th * std::pow(std::sqrt(x) + JNU_CST * std::pow(x, 1.0 / 6.0), 2.0) *
+           std::exp(-std::pow(x, 1.0 / 3.0));
+}
+
+} /* namespace grmo */
+
+using namespace grmo;
+
+/* ------------------------------------------------------------------------- */
+/* the model                                                                  */
+/* ------------------------------------------------------------------------- */
+struct grmo_model {
+    Header hdr{};
+    Units units{};
+    int photon_n = 0;
+    std::vector<double> fld[8]; /* rho, u, u1, u2, u3, b1, b2, b3 : [n1][n2] */
+    double bias_norm = 0, rh = 0, x1_min = 0, max_tau_scatt = 0, d_tau_k = 0;
+    std::vector<double> hotcross, k2, ftab, weight, nint, dndlnu_max;
+    std::vector<double> gcov_z, gcon_z, det_z; /* per zone: 16, 16, 1 */
+    grmo_spectrum spectrum[N_TH_BINS][N_E_BINS];
+    uint64_t n_created = 0, n_scatt = 0, n_recorded = 0, n_steps = 0;
+    int zone_x_1 = 0, zone_x_2 = -1;
+    /* emission state (harm_model.cpp:706-811 statics) */
+    struct Zone {
+        int x_1 = 0, x_2 = 0, num_to_gen = -1;
+        double dn_max = 0;
+        bool first_photon = true;
+    } zone;
+    Fluid ez_fluid{};
+    double ez_econ[4][4], ez_ecov[4][4];
+    std::mt19937 emit_mt;
+    uint64_t emit_seed = 0;
+    bool emit_started = false;
+    /* bias controls for batch tracking */
+    int bias_mode = GRMO_BIAS_LIVE;
+    uint64_t b_scatt0 = 0, b_rec0 = 0;
+    double b_maxtau0 = 0;
+    /* trace sink */
+    grmo_trace *trace = nullptr;
+    size_t trace_cap = 0;
+    int64_t trace_n = 0;
+
+    int n1() const { return hdr.n[0]; }
+    int n2() const { return hdr.n[1]; }
+    double F(int f, int i, int j) const { return fld[f][(size_t)i * hdr.n[1] + j]; }
+    double HC(int i, int j) const { return hotcross[(size_t)i * (HC_N_T + 1) + j]; }
+};
+
+/* harm_model.cpp:64-79 */
+static void model_units(grmo_model *m, double mass_unit) {
+    Units &u = m->units;
+    u.mass_unit = mass_unit;
+    u.l_unit = G_NEWT * M_BH / (CL * CL);
+    u.t_unit = u.l_unit / CL;
+    u.rho_unit = u.mass_unit / std::pow(u.l_unit, 3);
+    u.u_unit = u.rho_unit * CL * CL;
+    u.b_unit = CL * std::sqrt(4.0 * kPi * u.rho_unit);
+    u.n_e_unit = u.rho_unit / (MP + ME);
+    m->max_tau_scatt = 6.0 * u.l_unit * u.rho_unit * 0.4;
+    m->d_tau_k = 2.0 * kPi * u.l_unit / (ME * CL * CL / HBAR);
+    std::memset(m->spectrum, 0, sizeof(m->spectrum));
+}
+
+/* ------------------------------------------------------------------------- */
+/* metric: harm_model.cpp:473-530, 1632-1644                                  */
+/* ------------------------------------------------------------------------- */
+static inline void bl_coord(const grmo_model *m, const double x[4], double &r, double &th) {
+    r = std::exp(x[1]) + m->hdr.r_0;
+    th = kPi * x[2] + ((1.0 - m->hdr.h_slope) / 2.0) * std::sin(2.0 * kPi * x[2]);
+}
+
+static void gcon_func(const grmo_model *m, const double x[4], double g[4][4]) { /* :473-497 */
+    std::memset(g, 0, sizeof(double) * 16);
+    double r, th;
+    bl_coord(m, x, r, th);
+    const double a = m->hdr.a;
+    const double sin_theta = std::fabs(std::sin(th)) + EPS;
+    const double cos_theta = std::cos(th);
+    const double irho2 = 1.0 / (r * r + a * a * cos_theta * cos_theta);
+    const double hfac = kPi + (1.0 - m->hdr.h_slope) * kPi * std::cos(2.0 * kPi * x[2]);
+    g[0][0] = -1.0 - 2.0 * r * irho2;
+    g[0][1] = 2.0 * irho2;
+    g[1][0] = g[0][1];
+    g[1][1] = irho2 * (r * (r - 2.0) + a * a) / (r * r);
+    g[1][3] = a * irho2 / r;
+    g[2][2] = irho2 / (hfac * hfac);
+    g[3][1] = g[1][3];
+    g[3][3] = irho2 / (sin_theta * sin_theta);
+}
+
+static void gcov_func(const grmo_model *m, const double x[4], double g[4][4]) { /* :499-530 */
+    std::memset(g, 0, sizeof(double) * 16);
+    double r, th;
+    bl_coord(m, x, r, th);
+    const double a = m->hdr.a;
+    const double sin_theta = std::fabs(std::sin(th)) + EPS;
+    const double cos_theta = std::cos(th);
+    const double sin_theta_2 = sin_theta * sin_theta;
+    const double rho2 = r * r + a * a * cos_theta * cos_theta;
+    const double tfac = 1.0, pfac = 1.0;
+    const double rfac = r - m->hdr.r_0;
+    const double hfac = kPi + (1.0 - m->hdr.h_slope) * kPi * std::cos(2.0 * kPi * x[2]);
+    g[0][0] = (-1.0 + 2.0 * r / rho2) * tfac * tfac;
+    g[0][1] = (2.0 * r / rho2) * tfac * rfac;
+    g[0][3] = (-2.0 * a * r * sin_theta_2 / rho2) * tfac * pfac;
+    g[1][0] = g[0][1];
+    g[1][1] = (1.0 + 2.0 * r / rho2) * rfac * rfac;
+    g[1][3] = (-a * sin_theta_2 * (1.0 + 2.0 * r / rho2)) * rfac * pfac;
+    g[2][2] = rho2 * hfac * hfac;
+    g[3][0] = g[0][3];
+    g[3][1] = g[1][3];
+    g[3][3] = sin_theta_2 * (rho2 + a * a * sin_theta_2 * (1.0 + 2.0 * r / rho2)) * pfac * pfac;
+}
+
+static void coord_of(const grmo_model *m, int i, int j, double x[4]) { /* :1639-1644 */
+    x[0] = m->hdr.x_start[0];
+    x[1] = m->hdr.x_start[1] + (i + 0.5) * m->hdr.dx[1];
+    x[2] = m->hdr.x_start[2] + (j + 0.5) * m->hdr.dx[2];
+    x[3] = m->hdr.x_start[3];
+}
+
+/* Laplace expansion along row 0 (linalg.hpp det_4x4 semantics) */
+static double det4(const double a[16]) {
+    auto m3 = [&](int r0, int r1, int r2, int c0, int c1, int c2) {
+        return a[r0 * 4 + c0] * (a[r1 * 4 + c1] * a[r2 * 4 + c2] - a[r1 * 4 + c2] * a[r2 * 4 + c1]) -
+               a[r0 * 4 + c1] * (a[r1 * 4 + c0] * a[r2 * 4 + c2] - a[r1 * 4 + c2] * a[r2 * 4 + c0]) +
+               a[r0 * 4 + c2] * (a[r1 * 4 + c0] * a[r2 * 4 + c1] - a[r1 * 4 + c1] * a[r2 * 4 + c0]);
+    };
+    return a[0] * m3(1, 2, 3, 1, 2, 3) - a[1] * m3(1, 2, 3, 0, 2, 3) + a[2] * m3(1, 2, 3, 0, 1, 3) -
+           a[3] * m3(1, 2, 3, 0, 1, 2);
+}
+
+/* :1436-1569 -- analytic Christoffel symbols of MKS Kerr (only j<=k filled) */
+static void get_connection(const grmo_model *m, const double x[4], double L[4][4][4]) {
+    const double r1 = std::exp(x[1]);
+    const double r2 = r1 * r1, r3 = r2 * r1, r4 = r3 * r1;
+    const double s_x = std::sin(2.0 * kPi * x[2]);
+    const double c_x = std::cos(2.0 * kPi * x[2]);
+    const double hs = m->hdr.h_slope;
+    const double th = kPi * x[2] + 0.5 * (1.0 - hs) * s_x;
+    const double dthdx2 = kPi * (1.0 + (1.0 - hs) * c_x);
+    const double d2thdx22 = -2.0 * kPi * kPi * (1.0 - hs) * s_x;
+    const double dthdx22 = dthdx2 * dthdx2;
+    const double sth = std::sin(th), cth = std::cos(th);
+    const double sth2 = sth * sth, r1sth2 = r1 * sth2, sth4 = sth2 * sth2;
+    const double cth2 = cth * cth, cth4 = cth2 * cth2;
+    const double s2th = 2.0 * sth * cth, c2th = 2.0 * cth2 - 1.0;
+    const double a = m->hdr.a, a2 = a * a, a3 = a2 * a, a4 = a3 * a;
+    const double a2sth2 = a2 * sth2, a2cth2 = a2 * cth2, a4cth4 = a4 * cth4;
+    const double rho2 = r2 + a2cth2, rho22 = rho2 * rho2, rho23 = rho22 * rho2;
+    const double irho2 = 1.0 / rho2, irho22 = irho2 * irho2, irho23 = irho22 * irho2;
+    const double irho23_dthdx2 = irho23 / dthdx2;
+    const double fac1 = r2 - a2cth2, fac1_rho23 = fac1 * irho23;
+    const double fac2 = a2 + 2.0 * r2 + a2 * c2th;
+    const double fac3 = a2 + r1 * (-2.0 + r1);
+
+    L[0][0][0] = 2.0 * r1 * fac1_rho23;
+    L[0][0][1] = r1 * (2.0 * r1 + rho2) * fac1_rho23;
+    L[0][0][2] = -a2 * r1 * s2th * dthdx2 * irho22;
+    L[0][0][3] = -2.0 * a * r1sth2 * fac1_rho23;
+    L[0][1][1] = 2.0 * r2 * (r4 + r1 * fac1 - a4cth4) * irho23;
+    L[0][1][2] = -a2 * r2 * s2th * dthdx2 * irho22;
+    L[0][1][3] = a * r1 * (-r1 * (r3 + 2.0 * fac1) + a4cth4) * sth2 * irho23;
+    L[0][2][2] = -2.0 * r2 * dthdx22 * irho2;
+    L[0][2][3] = a3 * r1sth2 * s2th * dthdx2 * irho22;
+    L[0][3][3] = 2.0 * r1sth2 * (-r1 * rho22 + a2sth2 * fac1) * irho23;
+
+    L[1][0][0] = fac3 * fac1 / (r1 * rho23);
+    L[1][0][1] = fac1 * (-2.0 * r1 + a2sth2) * irho23;
+    L[1][0][2] = 0.0;
+    L[1][0][3] = -a * sth2 * fac3 * fac1 / (r1 * rho23);
+    L[1][1][1] = (r4 * (-2.0 + r1) * (1.0 + r1) +
+                  a2 * (a2 * r1 * (1.0 + 3.0 * r1) * cth4 + a4cth4 * cth2 + r3 * sth2 +
+                        r1 * cth2 * (2.0 * r1 + 3.0 * r3 - a2sth2))) *
+                 irho23;
+    L[1][1][2] = -a2 * dthdx2 * s2th / fac2;
+    L[1][1][3] = a * sth2 * (a4 * r1 * cth4 + r2 * (2.0 * r1 + r3 - a2sth2) + a2cth2 * (2.0 * r1 * (-1.0 + r2) + a2sth2)) *
+                 irho23;
+    L[1][2][2] = -fac3 * dthdx22 * irho2;
+    L[1][2][3] = 0.0;
+    L[1][3][3] = -fac3 * sth2 * (r1 * rho22 - a2 * fac1 * sth2) / (r1 * rho23);
+
+    L[2][0][0] = -a2 * r1 * s2th * irho23_dthdx2;
+    L[2][0][1] = r1 * L[2][0][0];
+    L[2][0][2] = 0.0;
+    L[2][0][3] = a * r1 * (a2 + r2) * s2th * irho23_dthdx2;
+    L[2][1][1] = r2 * L[2][0][0];
+    L[2][1][2] = r2 * irho2;
+    L[2][1][3] = (a * r1 * cth * sth * (r3 * (2.0 + r1) + a2 * (2.0 * r1 * (1.0 + r1) * cth2 + a2 * cth4 + 2.0 * r1sth2))) *
+                 irho23_dthdx2;
+    L[2][2][2] = -a2 * cth * sth * dthdx2 * irho2 + d2thdx22 / dthdx2;
+    L[2][2][3] = 0.0;
+    L[2][3][3] = -cth * sth * (rho23 + a2sth2 * rho2 * (r1 * (4.0 + r1) + a2cth2) + 2.0 * r1 * a4 * sth4) *
+                 irho23_dthdx2;
+
+    L[3][0][0] = a * fac1_rho23;
+    L[3][0][1] = r1 * L[3][0][0];
+    L[3][0][2] = -2.0 * a * r1 * cth * dthdx2 / (sth * rho22);
+    L[3][0][3] = -a2sth2 * fac1_rho23;
+    L[3][1][1] = a * r2 * fac1_rho23;
+    L[3][1][2] = -2 * a * r1 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * cth * dthdx2 / (sth * fac2 * fac2);
+    L[3][1][3] = r1 * (r1 * rho22 - a2sth2 * fac1) * irho23;
+    L[3][2][2] = -a * r1 * dthdx22 * irho2;
+    L[3][2][3] = dthdx2 * (0.25 * fac2 * fac2 * cth / sth + a2 * r1 * s2th) * irho22;
+    L[3][3][3] = (-a * r1sth2 * rho22 + a3 * sth4 * fac1) * irho23;
+}
+
+/* geodesic RHS, the common body of init_dkdlam (:1571-1587) and push_photon (:1255-1262) */
+static inline double geo_rhs(const double L[4][4][4], int i, const double k[4]) {
+    double d = -2.0 * (k[0] * (L[i][0][1] * k[1] + L[i][0][2] * k[2] + L[i][0][3] * k[3]) +
+                       k[1] * (L[i][1][2] * k[2] + L[i][1][3] * k[3]) + L[i][2][3] * k[2] * k[3]);
+    d -= (L[i][0][0] * k[0] * k[0] + L[i][1][1] * k[1] * k[1] + L[i][2][2] * k[2] * k[2] + L[i][3][3] * k[3] * k[3]);
+    return d;
+}
+
+static void init_dkdlam(const grmo_model *m, const double x[4], const double k[4], double dk[4]) {
+    double L[4][4][4];
+    get_connection(m, x, L);
+    for (int i = 0; i < 4; ++i) dk[i] = geo_rhs(L, i, k);
+}
+
+/* :1620-1630 */
+static double step_size(const grmo_model *m, const double x[4], const double k[4]) {
+    const double dl_x_1 = STEP_EPS * x[1] / (std::abs(k[1]) + EPS);
+    const double dl_x_2 = STEP_EPS * std::min(x[2], m->hdr.x_stop[2] - x[2]) / (std::abs(k[2]) + EPS);
+    const double dl_x_3 = STEP_EPS / (std::abs(k[3]) + EPS);
+    const double i1 = 1.0 / (std::abs(dl_x_1) + EPS);
+    const double i2 = 1.0 / (std::abs(dl_x_2) + EPS);
+    const double i3 = 1.0 / (std::abs(dl_x_3) + EPS);
+    return 1.0 / (i1 + i2 + i3);
+}
+
+/* instrumentation (test statistics only): push attempts, 2nd corrector iterations, halvings */
+static uint64_t g_dbg_attempts = 0, g_dbg_iter2 = 0, g_dbg_fail = 0;
+
+/* :1217-1289 -- second-order push with energy check and recursive halving */
+static void push_photon(const grmo_model *m, double x[4], double kv[4], double dkdlam[4], double &e_0_s, double dl,
+                        int n) {
+    if (x[1] < m->hdr.x_start[1]) return;
+    double x_cpy[4], k_cpy[4], dk_cpy[4];
+    for (int i = 0; i < 4; ++i) {
+        x_cpy[i] = x[i];
+        k_cpy[i] = kv[i];
+        dk_cpy[i] = dkdlam[i];
+    }
+    const double dl_2 = 0.5 * dl;
+    double kp[4];
+    for (int i = 0; i < 4; ++i) {
+        const double dk = dkdlam[i] * dl_2;
+        kv[i] += dk;
+        kp[i] = kv[i] + dk;
+        x[i] += kv[i] * dl;
+    }
+    double L[4][4][4];
+    get_connection(m, x, L);
+    double err;
+    int iter = 0;
+    ++g_dbg_attempts;
+    do {
+        ++iter;
+        double kc[4] = {kp[0], kp[1], kp[2], kp[3]};
+        err = 0.0;
+        for (int i = 0; i < 4; ++i) {
+            dkdlam[i] = geo_rhs(L, i, kc);
+            kp[i] = kv[i] + dl_2 * dkdlam[i];
+            err += std::abs((kc[i] - kp[i]) / (kp[i] + EPS));
+        }
+    } while (err > E_TOL && iter < MAX_ITER);
+    if (iter > 1) ++g_dbg_iter2;
+    for (int i = 0; i < 4; ++i) kv[i] = kp[i];
+    double g[4][4];
+    gcov_func(m, x, g);
+    double e_1 = -(kv[0] * g[0][0] + kv[1] * g[0][1] + kv[2] * g[0][2] + kv[3] * g[0][3]);
+    const double err_e = std::abs((e_1 - e_0_s) / e_0_s);
+    if (n < 7 && (err_e > 1.0e-4 || err > E_TOL || std::isnan(err) || std::isinf(err))) {
+        ++g_dbg_fail;
+        for (int i = 0; i < 4; ++i) {
+            x[i] = x_cpy[i];
+            kv[i] = k_cpy[i];
+            dkdlam[i] = dk_cpy[i];
+        }
+        push_photon(m, x, kv, dkdlam, e_0_s, 0.5 * dl, n + 1);
+        push_photon(m, x, kv, dkdlam, e_0_s, 0.5 * dl, n + 1);
+        e_1 = e_0_s;
+    }
+    e_0_s = e_1;
+}
+
+/* tetrads.cpp:126-155 */
+static inline void lower(const double u[4], const double g[4][4], double uc[4]) {
+    for (int i = 0; i < 4; ++i) uc[i] = g[i][0] * u[0] + g[i][1] * u[1] + g[i][2] * u[2] + g[i][3] * u[3];
+}
+
+/* :1406-1434 */
+static void x_to_ij(const grmo_model *m, const double x[4], int &i, int &j, double &di, double &dj) {
+    const Header &h = m->hdr;
+    i = (int)((x[1] - h.x_start[1]) / h.dx[1] - 0.5 + 1000) - 1000;
+    j = (int)((x[2] - h.x_start[2]) / h.dx[2] - 0.5 + 1000) - 1000;
+    if (i < 0) {
+        i = 0;
+        di = 0.0;
+    } else if (i > h.n[0] - 2) {
+        i = h.n[0] - 2;
+        di = 1.0;
+    } else {
+        di = (x[1] - ((i + 0.5) * h.dx[1] + h.x_start[1])) / h.dx[1];
+    }
+    if (j < 0) {
+        j = 0;
+        dj = 0.0;
+    } else if (j > h.n[1] - 2) {
+        j = h.n[1] - 2;
+        dj = 1.0;
+    } else {
+        dj = (x[2] - ((j + 0.5) * h.dx[2] + h.x_start[2])) / h.dx[2];
+    }
+}
+
+/* :595-671 (+ interp_scalar :1646-1656). Out-of-grid: n_e = 0, other fields zeroed. */
+static void fluid_params(const grmo_model *m, const double x[4], const double gc[4][4], Fluid &fp) {
+    std::memset(&fp, 0, sizeof(fp));
+    const Header &h = m->hdr;
+    if (x[1] < h.x_start[1] || x[1] > h.x_stop[1] || x[2] < h.x_start[2] || x[2] > h.x_stop[2]) {
+        fp.n_e = 0.0;
+        return;
+    }
+    int i, j;
+    double di, dj;
+    x_to_ij(m, x, i, j, di, dj);
+    const double c[4] = {(1.0 - di) * (1.0 - dj), (1.0 - di) * dj, di * (1.0 - dj), di * dj};
+    auto interp = [&](int f) {
+        return m->F(f, i, j) * c[0] + m->F(f, i, j + 1) * c[1] + m->F(f, i + 1, j) * c[2] + m->F(f, i + 1, j + 1) * c[3];
+    };
+    const double rho = interp(0);
+    const double uu = interp(1);
+    fp.n_e = rho * m->units.n_e_unit;
+    fp.theta_e = uu / rho * m->units.theta_e_unit;
+    const double bp[4] = {0.0, interp(5), interp(6), interp(7)};
+    const double vc[4] = {0.0, interp(2), interp(3), interp(4)};
+    double gn[4][4];
+    gcon_func(m, x, gn);
+    double vdv = 0.0;
+    for (int a = 1; a < 4; ++a)
+        for (int b = 1; b < 4; ++b) vdv += gc[a][b] * vc[a] * vc[b];
+    const double vfac = std::sqrt(-1.0 / gn[0][0] * (1.0 + std::abs(vdv)));
+    fp.u_con[0] = -vfac * gn[0][0];
+    for (int a = 1; a < 4; ++a) fp.u_con[a] = vc[a] - vfac * gn[0][a];
+    lower(fp.u_con, gc, fp.u_cov);
+    double udb = 0.0;
+    for (int a = 1; a < 4; ++a) udb += fp.u_cov[a] * bp[a];
+    fp.b_con[0] = udb;
+    for (int a = 1; a < 4; ++a) fp.b_con[a] = (bp[a] + fp.u_con[a] * udb) / fp.u_con[0];
+    lower(fp.b_con, gc, fp.b_cov);
+    fp.b = std::sqrt(fp.b_con[0] * fp.b_cov[0] + fp.b_con[1] * fp.b_cov[1] + fp.b_con[2] * fp.b_cov[2] +
+                     fp.b_con[3] * fp.b_cov[3]) *
+           m->units.b_unit;
+}
+
+/* :538-593 -- zone-centred fluid state from the cached geometry */
+static Fluid fluid_zone(const grmo_model *m, int i, int j) {
+    Fluid r;
+    std::memset(&r, 0, sizeof(r));
+    const size_t z = (size_t)i * m->n2() + j;
+    const double *gc = &m->gcov_z[z * 16];
+    const double *gn = &m->gcon_z[z * 16];
+    const double vc[4] = {0.0, m->F(2, i, j), m->F(3, i, j), m->F(4, i, j)};
+    const double b[4] = {0.0, m->F(5, i, j), m->F(6, i, j), m->F(7, i, j)};
+    r.n_e = m->F(0, i, j) * m->units.n_e_unit;
+    r.theta_e = (m->F(1, i, j) / r.n_e) * m->units.n_e_unit * m->units.theta_e_unit;
+    double vdv = 0.0;
+    for (int a = 1; a < 4; ++a)
+        for (int c = 1; c < 4; ++c) vdv += gc[a * 4 + c] * vc[a] * vc[c];
+    const double vfac = std::sqrt(-1.0 / gn[0] * (1.0 + std::abs(vdv)));
+    r.u_con[0] = -vfac * gn[0];
+    for (int a = 1; a < 4; ++a) r.u_con[a] = vc[a] - vfac * gn[a];
+    double g[4][4];
+    std::memcpy(g, gc, sizeof(g));
+    double uc[4], bc[4];
+    lower(r.u_con, g, uc);
+    double udb = 0.0;
+    for (int a = 1; a < 4; ++a) udb += uc[a] * b[a];
+    r.b_con[0] = udb;
+    for (int a = 1; a < 4; ++a) r.b_con[a] = (b[a] + r.u_con[a] * udb) / r.u_con[0];
+    lower(r.b_con, g, bc);
+    r.b = std::sqrt(r.b_con[0] * bc[0] + r.b_con[1] * bc[1] + r.b_con[2] * bc[2] + r.b_con[3] * bc[3]) *
+          m->units.b_unit;
+    std::memcpy(r.u_cov, uc, sizeof(uc));
+    std::memcpy(r.b_cov, bc, sizeof(bc));
+    return r;
+}
+
+/* ------------------------------------------------------------------------- */
+/* radiation.cpp:59-146, hotcross.cpp:81-106, jnu_mixed.cpp:75-158            */
+/* ------------------------------------------------------------------------- */
+static double hotcross_lkup(const grmo_model *m, double w, double theta_e) {
+    if (w * theta_e < 1.0e-6) return SIGMA_THOMSON;
+    if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
+    if (w <= HC_MIN_W || w >= HC_MAX_W || theta_e <= HC_MIN_T || theta_e >= HC_MAX_T) return hotcross_num(w, theta_e);
+    const double l_w = std::log10(w), l_t = std::log10(theta_e);
+    const int i = (int)((l_w - D.hc_l_min_w) / D.hc_d_l_w);
+    const int j = (int)((l_t - D.hc_l_min_t) / D.hc_d_l_t);
+    const double d_i = (l_w - D.hc_l_min_w) / D.hc_d_l_w - i;
+    const double d_j = (l_t - D.hc_l_min_t) / D.hc_d_l_t - j;
+    const double lc = (1.0 - d_i) * (1.0 - d_j) * m->HC(i, j) + d_i * (1.0 - d_j) * m->HC(i + 1, j) +
+                      (1.0 - d_i) * d_j * m->HC(i, j + 1) + d_i * d_j * m->HC(i + 1, j + 1);
+    return std::pow(10, lc);
+}
+
+static double k2_eval(const grmo_model *m, double theta_e) { /* jnu_mixed.cpp:102-111, 150-158 */
+    if (theta_e < THETA_E_MIN) return 0.0;
+    if (theta_e > JNU_MAX_T) return 2.0 * theta_e * theta_e;
+    const double l_t = std::log(theta_e);
+    double d_i = (l_t - D.jnu_l_min_t) / D.jnu_d_l_t;
+    const int i = (int)d_i;
+    d_i -= i;
+    return std::exp((1.0 - d_i) * m->k2[i] + d_i * m->k2[i + 1]);
+}
+
+static double f_eval(const grmo_model *m, double theta_e, double b_mag, double nu) { /* jnu_mixed.cpp:113-125 */
+    const double k = JNU_K_FAC * nu / (b_mag * theta_e * theta_e);
+    if (k > JNU_MAX_K) return 0.0;
+    if (k < JNU_MIN_K) {
+        const double x = std::pow(k, 1.0 / 3.0);
+        return x * (37.67503800178 + 2.240274341836 * x);
+    }
+    const double l_k = std::log(k);
+    double d_i = (l_k - D.jnu_l_min_k) / D.jnu_d_l_k;
+    const int i = (int)d_i;
+    d_i -= i;
+    return std::exp((1.0 - d_i) * m->ftab[i] + d_i * m->ftab[i + 1]);
+}
+
+static double synch(const grmo_model *m, double nu, double n_e, double theta_e, double b, double theta) {
+    if (theta_e < THETA_E_MIN) return 0.0; /* jnu_mixed.cpp:75-100 */
+    const double k2 = k2_eval(m, theta_e);
+    const double nu_c = EE * b / (2.0 * kPi * ME * CL);
+    const double sin_th = std::sin(theta);
+    const double nu_s = (2.0 / 9.0) * nu_c * theta_e * theta_e * sin_th;
+    if (nu > 1.0e12 * nu_s) return 0.0;
+    const double x = nu / nu_s;
+    const double xp = std::pow(x, 1.0 / 3.0);
+    const double xx = std::sqrt(x) + JNU_CST * std::sqrt(xp);
+    const double f = xx * xx;
+    return (kSqrt2 * kPi * EE * EE * n_e * nu_s / (3.0 * CL * k2)) * f * std::exp(-xp);
+}
+
+static double bk_angle(const double k[4], const double u_cov[4], const double b_cov[4], double b, double b_unit) {
+    if (b == 0.0) return kPi / 2.0; /* radiation.cpp:59-87 */
+    const double k_ = std::abs(k[0] * u_cov[0] + k[1] * u_cov[1] + k[2] * u_cov[2] + k[3] * u_cov[3]);
+    double mu = (k[0] * b_cov[0] + k[1] * b_cov[1] + k[2] * b_cov[2] + k[3] * b_cov[3]) / (k_ * b / b_unit);
+    mu = std::clamp(mu, -1.0, 1.0);
+    return std::acos(mu);
+}
+
+static double fluid_nu(const double k[4], const double u_cov[4]) { /* radiation.cpp:89-101 */
+    const double energy = -(k[0] * u_cov[0] + k[1] * u_cov[1] + k[2] * u_cov[2] + k[3] * u_cov[3]);
+    return energy * ME * CL * CL / HPL;
+}
+
+static double alpha_inv_scatt(const grmo_model *m, double nu, double theta_e, double n_e) { /* :103-107,142-146 */
+    const double e_g = HPL * nu / (ME * CL * CL);
+    const double kappa = hotcross_lkup(m, e_g, theta_e) / MP;
+    return nu * kappa * n_e * MP;
+}
+
+static double alpha_inv_abs(const grmo_model *m, double nu, double theta_e, double n_e, double b, double theta) {
+    const double j = synch(m, nu, n_e, theta_e, b, theta) / (nu * nu); /* radiation.cpp:109-140 */
+    const double x = HPL * nu / (ME * CL * CL * theta_e);
+    double b_nu;
+    if (x < 1.0e-3)
+        b_nu = (2.0 * HPL / (CL * CL)) / (x / 24.0 * (24.0 + x * (12.0 + x * (4.0 + x))));
+    else
+        b_nu = (2.0 * HPL / (CL * CL)) / (std::exp(x) - 1.0);
+    return j / (b_nu + 1.0e-100);
+}
+
+/* ------------------------------------------------------------------------- */
+/* tetrads.cpp:46-194                                                         */
+/* ------------------------------------------------------------------------- */
+static void t_normalize(double v[4], const double g[4][4]) {
+    double norm = 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) norm += v[i] * v[j] * g[i][j];
+    norm = std::sqrt(std::abs(norm));
+    for (int i = 0; i < 4; ++i) v[i] /= norm;
+}
+
+static void t_project_out(double va[4], const double vb[4], const double g[4][4]) {
+    double bsq = 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) bsq += vb[i] * vb[j] * g[i][j];
+    double adb = 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) adb += va[i] * vb[j] * g[i][j];
+    for (int i = 0; i < 4; ++i) va[i] -= vb[i] * adb / bsq;
+}
+
+static void make_tetrad(const double u_con[4], double trial[4], const double g[4][4], double ec[4][4],
+                        double el[4][4]) {
+    for (int i = 0; i < 4; ++i) ec[0][i] = u_con[i];
+    t_normalize(ec[0], g);
+    double norm = 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) norm += trial[i] * trial[j] * g[i][j];
+    if (norm < 1.0e-30)
+        for (int i = 0; i < 4; ++i) trial[i] = (i == 1) ? 1.0 : 0.0;
+    for (int i = 0; i < 4; ++i) ec[1][i] = trial[i];
+    t_project_out(ec[1], ec[0], g);
+    t_normalize(ec[1], g);
+    for (int i = 0; i < 4; ++i) ec[2][i] = (i == 2) ? 1.0 : 0.0;
+    t_project_out(ec[2], ec[0], g);
+    t_project_out(ec[2], ec[1], g);
+    t_normalize(ec[2], g);
+    for (int i = 0; i < 4; ++i) ec[3][i] = (i == 3) ? 1.0 : 0.0;
+    t_project_out(ec[3], ec[0], g);
+    t_project_out(ec[3], ec[1], g);
+    t_project_out(ec[3], ec[2], g);
+    t_normalize(ec[3], g);
+    for (int i = 0; i < 4; ++i) lower(ec[i], g, el[i]);
+    for (int i = 0; i < 4; ++i) el[0][i] *= -1.0;
+}
+
+static void coord_to_tetrad(const double el[4][4], const double k[4], double kt[4]) {
+    for (int i = 0; i < 4; ++i) {
+        kt[i] = 0.0;
+        for (int j = 0; j < 4; ++j) kt[i] += el[i][j] * k[j];
+    }
+}
+
+static void tetrad_to_coord(const double ec[4][4], const double kt[4], double k[4]) {
+    for (int i = 0; i < 4; ++i) {
+        k[i] = 0.0;
+        for (int j = 0; j < 4; ++j) k[i] += ec[j][i] * kt[j];
+    }
+}
+
+/* harm_model.cpp:1658-1671 */
+static void boost(const double v[4], const double u[4], double vp[4]) {
+    const double g = u[0];
+    const double v_ = std::sqrt(std::abs(1.0 - 1.0 / (g * g)));
+    const double n1 = u[1] / (g * v_ + EPS), n2 = u[2] / (g * v_ + EPS), n3 = u[3] / (g * v_ + EPS);
+    const double gm1 = g - 1.0;
+    vp[0] = u[0] * v[0] - u[1] * v[1] - u[2] * v[2] - u[3] * v[3];
+    vp[1] = -u[1] * v[0] + (1.0 + n1 * n1 * gm1) * v[1] + n1 * n2 * gm1 * v[2] + n1 * n3 * gm1 * v[3];
+    vp[2] = -u[2] * v[0] + n2 * n1 * gm1 * v[1] + (1.0 + n2 * n2 * gm1) * v[2] + n2 * n3 * gm1 * v[3];
+    vp[3] = -u[3] * v[0] + n3 * n1 * gm1 * v[1] + n3 * n2 * gm1 * v[2] + (1.0 + n3 * n3 * gm1) * v[3];
+}
+
+/* ------------------------------------------------------------------------- */
+/* proba.cpp:30-215                                                           */
+/* ------------------------------------------------------------------------- */
+/* The reference build evaluates sin and cos of the azimuth with two separate libm calls
+ * (no sincos merge); glibc's sincos can differ from them in the last bit, so keep them separate. */
+static __attribute__((noinline)) double sep_sin(double v) { return std::sin(v); }
+static __attribute__((noinline)) double sep_cos(double v) { return std::cos(v); }
+
+static void sample_rand_dir(Rng &r, double &x, double &y, double &z) { /* :202-210 */
+    z = r.uniform() * 2.0 - 1.0;
+    const double phi = r.uniform() * 2.0 * kPi;
+    x = std::sqrt(1.0 - z * z) * sep_cos(phi);
+    y = std::sqrt(1.0 - z * z) * sep_sin(phi);
+}
+
+static double sample_y_distr(Rng &r, double theta_e) { /* :123-166 */
+    double pi_3 = std::sqrt(kPi) / 4.0;
+    double pi_4 = std::sqrt(0.5 * theta_e) / 2.0;
+    double pi_5 = 3.0 * std::sqrt(kPi) * theta_e / 8.0;
+    double pi_6 = theta_e * std::sqrt(0.5 * theta_e);
+    const double s_3 = pi_3 + pi_4 + pi_5 + pi_6;
+    pi_3 /= s_3;
+    pi_4 /= s_3;
+    pi_5 /= s_3;
+    pi_6 /= s_3;
+    double y, x2, prob;
+    do {
+        const double x1 = r.uniform();
+        int dof;
+        if (x1 < pi_3)
+            dof = 3;
+        else if (x1 < pi_3 + pi_4)
+            dof = 4;
+        else if (x1 < pi_3 + pi_4 + pi_5)
+            dof = 5;
+        else
+            dof = 6;
+        const double x = r.chi_sq(dof);
+        y = std::sqrt(x / 2.0);
+        x2 = r.uniform();
+        const double num = std::sqrt(1.0 + 0.5 * theta_e * y * y);
+        const double den = (1.0 + y * std::sqrt(0.5 * theta_e));
+        prob = num / den;
+    } while (x2 >= prob);
+    return y;
+}
+
+static double sample_mu_distr(Rng &r, double beta_e) { /* :168-172 */
+    const double x1 = r.uniform();
+    const double det = 1.0 + 2.0 * beta_e + beta_e * beta_e - 4.0 * beta_e * x1;
+    return (1.0 - std::sqrt(det)) / beta_e;
+}
+
+static void sample_electron(Rng &r, const double k[4], double p[4], double theta_e) { /* :30-112 */
+    double sigma_kn, gamma_e, beta_e, mu, x1;
+    do {
+        const double y = sample_y_distr(r, theta_e); /* sample_beta_distr :114-121 */
+        gamma_e = y * y * theta_e + 1.0;
+        beta_e = std::sqrt(1.0 - 1.0 / (gamma_e * gamma_e));
+        mu = sample_mu_distr(r, beta_e);
+        if (mu > 1.0)
+            mu = 1.0;
+        else if (mu < -1.0)
+            mu = -1.0;
+        const double k_ = gamma_e * (1.0 - beta_e * mu) * k[0];
+        if (k_ < 1.0e-3)
+            sigma_kn = 1.0 - 2.0 * k_;
+        else
+            sigma_kn = (3.0 / (4.0 * k_ * k_)) * (2.0 + k_ * k_ * (1.0 + k_) / ((1.0 + 2.0 * k_) * (1.0 + 2.0 * k_)) +
+                                                  (k_ * k_ - 2.0 * k_ - 2.0) / (2.0 * k_) * std::log(1.0 + 2.0 * k_));
+        x1 = r.uniform();
+    } while (x1 >= sigma_kn);
+    double v0x = k[1], v0y = k[2], v0z = k[3];
+    const double v0 = std::sqrt(v0x * v0x + v0y * v0y + v0z * v0z);
+    v0x /= v0;
+    v0y /= v0;
+    v0z /= v0;
+    double n0x, n0y, n0z;
+    sample_rand_dir(r, n0x, n0y, n0z);
+    const double n0dotv0 = v0x * n0x + v0y * n0y + v0z * n0z;
+    double v1x = n0x - (n0dotv0)*v0x, v1y = n0y - (n0dotv0)*v0y, v1z = n0z - (n0dotv0)*v0z;
+    const double v1 = std::sqrt(v1x * v1x + v1y * v1y + v1z * v1z);
+    v1x /= v1;
+    v1y /= v1;
+    v1z /= v1;
+    const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
+    const double phi = r.uniform() * 2.0 * kPi;
+    const double s_phi = std::sin(phi), c_phi = std::cos(phi);
+    const double c_th = mu, s_th = std::sqrt(1. - mu * mu);
+    p[0] = gamma_e;
+    p[1] = gamma_e * beta_e * (c_th * v0x + s_th * (c_phi * v1x + s_phi * v2x));
+    p[2] = gamma_e * beta_e * (c_th * v0y + s_th * (c_phi * v1y + s_phi * v2y));
+    p[3] = gamma_e * beta_e * (c_th * v0z + s_th * (c_phi * v1z + s_phi * v2z));
+}
+
+static double kn_xsec(double a, double ap) { /* :212-215 */
+    const double ch = 1.0 + 1.0 / a - 1.0 / ap;
+    return (a / ap + ap / a - 1.0 + ch * ch) / (a * a);
+}
+
+static double sample_klein_nishina(Rng &r, double k0) { /* :174-189 */
+    const double k0pmin = k0 / (1.0 + 2.0 * k0), k0pmax = k0;
+    double x1, k0p_tent;
+    do {
+        k0p_tent = k0pmin + (k0pmax - k0pmin) * r.uniform();
+        x1 = 2.0 * (1.0 + 2.0 * k0 + 2.0 * k0 * k0) / (k0 * k0 * (1.0 + 2.0 * k0));
+        x1 *= r.uniform();
+    } while (x1 >= kn_xsec(k0, k0p_tent));
+    return k0p_tent;
+}
+
+static double sample_thomson(Rng &r) { /* :191-200 */
+    double x1, x2;
+    do {
+        x1 = 2.0 * r.uniform() - 1.0;
+        x2 = (3.0 / 4.0) * r.uniform();
+    } while (x2 >= (3.0 / 8.0) * (1.0 + x1 * x1));
+    return x1;
+}
+
+/* harm_model.cpp:1147-1215 */
+static void sample_scattered(Rng &r, const double k[4], double p[4], double kp[4]) {
+    double ke[4];
+    boost(k, p, ke);
+    double k0p, c_th;
+    if (ke[0] > 1.0e-4) {
+        k0p = sample_klein_nishina(r, ke[0]);
+        c_th = 1.0 - 1.0 / k0p + 1.0 / ke[0];
+    } else {
+        k0p = ke[0];
+        c_th = sample_thomson(r);
+    }
+    const double s_th = std::sqrt(std::abs(1.0 - c_th * c_th));
+    const double v0x = ke[1] / ke[0], v0y = ke[2] / ke[0], v0z = ke[3] / ke[0];
+    double n0x, n0y, n0z;
+    sample_rand_dir(r, n0x, n0y, n0z);
+    const double n0dotv0 = v0x * n0x + v0y * n0y + v0z * n0z;
+    double v1x = n0x - (n0dotv0)*v0x, v1y = n0y - (n0dotv0)*v0y, v1z = n0z - (n0dotv0)*v0z;
+    const double v1 = std::sqrt(v1x * v1x + v1y * v1y + v1z * v1z);
+    v1x /= v1;
+    v1y /= v1;
+    v1z /= v1;
+    const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
+    const double phi = 2.0 * kPi * r.uniform();
+    const double s_phi = std::sin(phi), c_phi = std::cos(phi);
+    p[1] *= -1.;
+    p[2] *= -1.;
+    p[3] *= -1.;
+    const double d1 = c_th * v0x + s_th * (c_phi * v1x + s_phi * v2x);
+    const double d2 = c_th * v0y + s_th * (c_phi * v1y + s_phi * v2y);
+    const double d3 = c_th * v0z + s_th * (c_phi * v1z + s_phi * v2z);
+    const double kpe[4] = {k0p, k0p * d1, k0p * d2, k0p * d3};
+    boost(kpe, p, kp);
+}
+
+/* ------------------------------------------------------------------------- */
+/* transport: harm_model.cpp:894-1145, 1291-1335, 1391-1404, 1589-1618       */
+/* ------------------------------------------------------------------------- */
+static double bias_func(const grmo_model *m, double t_e, double w) {
+    const double max = 0.5 * w / WEIGHT_MIN;
+    double scatt = (double)m->n_scatt, rec = (double)m->n_recorded, mts = m->max_tau_scatt;
+    if (m->bias_mode == GRMO_BIAS_FROZEN) {
+        scatt = (double)m->b_scatt0;
+        rec = (double)m->b_rec0;
+        mts = m->b_maxtau0;
+    }
+    const double avg = scatt / (1.0 * rec + 1.0);
+    double bias = 100.0 * t_e * t_e / (m->bias_norm * mts * (avg + 2.0));
+    if (bias < TP_OVER_TE) bias = TP_OVER_TE;
+    if (bias > max) bias = max;
+    return bias / TP_OVER_TE;
+}
+
+static bool stop_criterion(const grmo_model *m, Photon &ph, Rng &r) {
+    if (ph.x[1] < m->x1_min) return true;
+    if (ph.x[1] > D.x1_max) {
+        if (ph.w < WEIGHT_MIN) {
+            if (r.uniform() <= 1.0 / ROULETTE)
+                ph.w *= ROULETTE;
+            else
+                ph.w = 0.0;
+        }
+        return true;
+    }
+    if (ph.w < WEIGHT_MIN) {
+        if (r.uniform() <= 1.0 / ROULETTE) {
+            ph.w *= ROULETTE;
+        } else {
+            ph.w = 0.0;
+            return true;
+        }
+    }
+    return false;
+}
+
+static void emit_trace(grmo_model *m, const Photon &ph, int n_step, int reason, int ix2, int i_e) {
+    if (!m->trace) return;
+    const int64_t t = m->trace_n++;
+    if ((size_t)t >= m->trace_cap) return;
+    grmo_trace &tr = m->trace[t];
+    tr.id = ph.id;
+    tr.parent_id = ph.parent_id;
+    tr.w = ph.w;
+    tr.e = ph.e;
+    tr.x1 = ph.x[1];
+    tr.x2 = ph.x[2];
+    tr.x3 = ph.x[3];
+    tr.tau_abs = ph.tau_abs;
+    tr.tau_scatt = ph.tau_scatt;
+    tr.n_scatt = ph.n_scatt;
+    tr.n_step = n_step;
+    tr.end_reason = reason;
+    tr.ix2 = ix2;
+    tr.i_e = i_e;
+    tr.pad_ = 0;
+}
+
+/* :1291-1335; returns true if binned */
+static bool record_super_photon(grmo_model *m, const Photon &ph, int &ix2_o, int &ie_o) {
+    ix2_o = -1;
+    ie_o = -1;
+    if (std::isnan(ph.w) || std::isnan(ph.e)) return false;
+    if (ph.tau_scatt > m->max_tau_scatt) m->max_tau_scatt = ph.tau_scatt;
+    const Header &h = m->hdr;
+    const double dx2 = (h.x_stop[2] - h.x_start[2]) / (2.0 * N_TH_BINS);
+    int ix2;
+    if (ph.x[2] < 0.5 * (h.x_start[2] + h.x_stop[2]))
+        ix2 = (int)(ph.x[2] / dx2);
+    else
+        ix2 = (int)((h.x_stop[2] - ph.x[2]) / dx2);
+    if (ix2 < 0 || ix2 >= N_TH_BINS) return false;
+    const double l_e = std::log(ph.e);
+    const int i_e = (int)((l_e - D.spec_l_e_0) / SPEC_D_L_E + 2.5) - 2;
+    if (i_e < 0 || i_e >= N_E_BINS) return false;
+    ix2_o = ix2;
+    ie_o = i_e;
+    ++m->n_recorded;
+    m->n_scatt += ph.n_scatt;
+    grmo_spectrum &s = m->spectrum[ix2][i_e];
+    s.dn_dle += ph.w;
+    s.de_dle += ph.w * ph.e;
+    s.tau_abs += ph.w * ph.tau_abs;
+    s.tau_scatt += ph.w * ph.tau_scatt;
+    s.x1i_av += ph.w * ph.x1i;
+    s.x2i_sq += ph.w * (ph.x2i * ph.x2i);
+    s.x3f_sq += ph.w * (ph.x[3] * ph.x[3]);
+    s.ne_0 += ph.w * (ph.n_e_0);
+    s.b_0 += ph.w * (ph.b_0);
+    s.theta_e_0 += ph.w * (ph.theta_e_0);
+    s.nscatt += ph.n_scatt;
+    s.nph += 1.0;
+    return true;
+}
+
+/* :1071-1145.  Returns: 0 ok (child valid), 1 parent killed (w=0), 2 child invalid. */
+static int scatter_super_photon(const grmo_model *m, Photon &ph, Photon &pc, const Fluid &fp, const double g[4][4],
+                                Rng &r) {
+    if (ph.k[0] > 1.0e5 || ph.k[0] < 0.0 || std::isnan(ph.k[0]) || std::isnan(ph.k[1]) || std::isnan(ph.k[3])) {
+        ph.k[0] = std::abs(ph.k[0]);
+        ph.w = 0.0;
+        return 1;
+    }
+    double bh[4];
+    if (fp.b > 0.0) {
+        for (int i = 0; i < 4; ++i) bh[i] = fp.b_con[i] / (fp.b / m->units.b_unit);
+    } else {
+        for (int i = 0; i < 4; ++i) bh[i] = 0.0;
+        bh[1] = 1.0;
+    }
+    double ec[4][4], el[4][4];
+    make_tetrad(fp.u_con, bh, g, ec, el);
+    double kt[4];
+    coord_to_tetrad(el, ph.k, kt);
+    if (kt[0] > 1.0e5 || kt[0] < 0.0 || std::isnan(kt[1])) return 2;
+    double p[4];
+    sample_electron(r, kt, p, fp.theta_e);
+    double ktp[4];
+    sample_scattered(r, kt, p, ktp);
+    tetrad_to_coord(ec, ktp, pc.k);
+    if (std::isnan(pc.k[1])) {
+        pc.w = 0.0;
+        return 2;
+    }
+    double tmp[4];
+    ktp[0] *= -1.0;
+    tetrad_to_coord(el, ktp, tmp);
+    pc.e = -tmp[0];
+    pc.e_0_s = -tmp[0];
+    pc.l = tmp[3];
+    pc.tau_abs = 0.0;
+    pc.tau_scatt = 0.0;
+    pc.b_0 = fp.b;
+    pc.x1i = ph.x[1];
+    pc.x2i = ph.x[2];
+    for (int i = 0; i < 4; ++i) pc.x[i] = ph.x[i];
+    pc.n_e_0 = ph.n_e_0;
+    pc.theta_e_0 = ph.theta_e_0;
+    pc.e_0 = ph.e_0;
+    pc.n_scatt = ph.n_scatt + 1;
+    return 0;
+}
+
+struct TrackCtx {
+    grmo_model *m;
+    int rng_mode;
+    uint64_t seed;
+    std::mt19937 *mt;
+};
+
+static void track_super_photon(TrackCtx &C, Photon &ph, Rng &rng) { /* :894-1069 */
+    grmo_model *m = C.m;
+    if (std::isnan(ph.x[0]) || std::isnan(ph.x[1]) || std::isnan(ph.x[2]) || std::isnan(ph.x[3]) ||
+        std::isnan(ph.k[0]) || std::isnan(ph.k[1]) || std::isnan(ph.k[2]) || std::isnan(ph.k[3]) || ph.w == 0.0) {
+        emit_trace(m, ph, 0, 4, -1, -1);
+        return;
+    }
+    double g[4][4];
+    gcov_func(m, ph.x, g);
+    Fluid fp;
+    fluid_params(m, ph.x, g, fp);
+    double theta = bk_angle(ph.k, fp.u_cov, fp.b_cov, fp.b, m->units.b_unit);
+    double nu = fluid_nu(ph.k, fp.u_cov);
+    double alpha_scatti = alpha_inv_scatt(m, nu, fp.theta_e, fp.n_e);
+    double alpha_absi = alpha_inv_abs(m, nu, fp.theta_e, fp.n_e, fp.b, theta);
+    double bi = bias_func(m, fp.theta_e, ph.w);
+    init_dkdlam(m, ph.x, ph.k, ph.dkdlam);
+    int n_step = 0;
+    int reason = 2;
+    while (!stop_criterion(m, ph, rng)) {
+        double x2[4], k2[4], dk2[4], e0s2 = ph.e_0_s;
+        for (int i = 0; i < 4; ++i) {
+            x2[i] = ph.x[i];
+            k2[i] = ph.k[i];
+            dk2[i] = ph.dkdlam[i];
+        }
+        const double dl = step_size(m, ph.x, ph.k);
+        push_photon(m, ph.x, ph.k, ph.dkdlam, ph.e_0_s, dl, 0);
+        m->n_steps++;
+        if (stop_criterion(m, ph, rng)) break;
+        if (alpha_absi > 0.0 || alpha_scatti > 0.0 || fp.n_e > 0.0) {
+            gcov_func(m, ph.x, g);
+            fluid_params(m, ph.x, g, fp);
+            const bool bound_flag = fp.n_e == 0.0;
+            if (!bound_flag) {
+                theta = bk_angle(ph.k, fp.u_cov, fp.b_cov, fp.b, m->units.b_unit);
+                nu = fluid_nu(ph.k, fp.u_cov);
+            }
+            double d_tau_scatt, d_tau_abs, bias;
+            if (bound_flag || nu < 0.0) {
+                d_tau_scatt = 0.5 * alpha_scatti * m->d_tau_k * dl;
+                d_tau_abs = 0.5 * alpha_absi * m->d_tau_k * dl;
+                alpha_scatti = 0.0;
+                alpha_absi = 0.0;
+                bias = 0.0;
+                bi = 0.0;
+            } else {
+                const double alpha_scattf = alpha_inv_scatt(m, nu, fp.theta_e, fp.n_e);
+                d_tau_scatt = 0.5 * (alpha_scatti + alpha_scattf) * m->d_tau_k * dl;
+                alpha_scatti = alpha_scattf;
+                const double alpha_absf = alpha_inv_abs(m, nu, fp.theta_e, fp.n_e, fp.b, theta);
+                d_tau_abs = 0.5 * (alpha_absi + alpha_absf) * m->d_tau_k * dl;
+                alpha_absi = alpha_absf;
+                const double bf = bias_func(m, fp.theta_e, ph.w);
+                bias = 0.5 * (bi + bf);
+                bi = bf;
+            }
+            const double x1 = -std::log(rng.uniform());
+            Photon pc;
+            std::memset(&pc, 0, sizeof(pc));
+            pc.w = ph.w / bias;
+            if (bias * d_tau_scatt > x1 && pc.w > WEIGHT_MIN) {
+                const double frac = x1 / (bias * d_tau_scatt);
+                d_tau_abs *= frac;
+                if (d_tau_abs > 100) {
+                    emit_trace(m, ph, n_step, 2, -1, -1);
+                    return; /* absorbed before scattering */
+                }
+                d_tau_scatt *= frac;
+                const double d_tau = d_tau_abs + d_tau_scatt;
+                if (d_tau_abs < 1.0e-3)
+                    ph.w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+                else
+                    ph.w *= std::exp(-d_tau);
+                push_photon(m, x2, k2, dk2, e0s2, dl * frac, 0);
+                for (int i = 0; i < 4; ++i) {
+                    ph.x[i] = x2[i];
+                    ph.k[i] = k2[i];
+                    ph.dkdlam[i] = dk2[i];
+                }
+                ph.e_0_s = e0s2;
+                gcov_func(m, ph.x, g);
+                fluid_params(m, ph.x, g, fp);
+                if (fp.n_e > 0.0) {
+                    /* child stream: device definition; MT mode shares the reference's global stream */
+                    Rng crng;
+                    uint64_t cid = 0;
+                    if (C.rng_mode == GRMO_RNG_PHILOX) {
+                        cid = child_id(ph.id, rng.ctr);
+                        crng = Rng::philox(C.seed, cid);
+                    }
+                    Rng &sr = (C.rng_mode == GRMO_RNG_PHILOX) ? crng : rng;
+                    const int st = scatter_super_photon(m, ph, pc, fp, g, sr);
+                    if (ph.w < 1.0e-100) {
+                        emit_trace(m, ph, n_step, 2, -1, -1);
+                        return;
+                    }
+                    pc.id = cid;
+                    pc.parent_id = ph.id;
+                    if (st == 0) {
+                        track_super_photon(C, pc, sr);
+                    } else {
+                        emit_trace(m, pc, 0, 4, -1, -1);
+                    }
+                }
+                theta = bk_angle(ph.k, fp.u_cov, fp.b_cov, fp.b, m->units.b_unit);
+                nu = fluid_nu(ph.k, fp.u_cov);
+                if (nu < 0.0) {
+                    alpha_scatti = 0.0;
+                    alpha_absi = 0.0;
+                } else {
+                    alpha_scatti = alpha_inv_scatt(m, nu, fp.theta_e, fp.n_e);
+                    alpha_absi = alpha_inv_abs(m, nu, fp.theta_e, fp.n_e, fp.b, theta);
+                }
+                bi = bias_func(m, fp.theta_e, ph.w);
+            } else {
+                if (d_tau_abs > 100) {
+                    emit_trace(m, ph, n_step, 2, -1, -1);
+                    return; /* absorbed */
+                }
+                const double d_tau = d_tau_abs + d_tau_scatt;
+                if (d_tau < 1.0e-3)
+                    ph.w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
+                else
+                    ph.w *= std::exp(-d_tau);
+            }
+            ph.tau_abs += d_tau_abs;
+            ph.tau_scatt += d_tau_scatt;
+        }
+        ++n_step;
+        if (n_step > MAX_N_STEP) {
+            reason = 3;
+            break;
+        }
+    }
+    if (ph.x[1] > D.x1_max && n_step <= MAX_N_STEP) {
+        int ix2, ie;
+        const bool binned = record_super_photon(m, ph, ix2, ie);
+        emit_trace(m, ph, n_step, binned ? 0 : 1, ix2, ie);
+    } else {
+        emit_trace(m, ph, n_step, reason, -1, -1);
+    }
+}
+
+static Photon from_init(const grmo_init_photon &ip) { /* harm_model.cpp:373-391 */
+    Photon p;
+    std::memset(&p, 0, sizeof(p));
+    for (int i = 0; i < 4; ++i) {
+        p.x[i] = ip.x[i];
+        p.k[i] = ip.k[i];
+    }
+    p.w = ip.w;
+    p.e = ip.e;
+    p.e_0 = ip.e_0;
+    p.e_0_s = ip.e;
+    p.l = ip.l;
+    p.tau_scatt = 0.0;
+    p.tau_abs = 0.0;
+    p.x1i = ip.x[1];
+    p.x2i = ip.x[2];
+    p.n_e_0 = ip.n_e_0;
+    p.b_0 = ip.b_0;
+    p.theta_e_0 = ip.theta_e_0;
+    p.n_scatt = 0;
+    return p;
+}
+
+/* ------------------------------------------------------------------------- */
+/* dump reader: harm_model.cpp:81-232                                         */
+/* ------------------------------------------------------------------------- */
+static int read_dump(grmo_model *m, const char *path) {
+    FILE *fp = std::fopen(path, "r");
+    if (!fp) return -1;
+    Header &h = m->hdr;
+    std::memset(&h, 0, sizeof(h));
+    auto rd = [&](double &v) { return std::fscanf(fp, "%lf", &v) == 1; };
+    auto ri = [&](int &v) {
+        double t;
+        if (std::fscanf(fp, "%lf", &t) != 1) return false;
+        v = (int)t;
+        return true;
+    };
+    bool ok = rd(h.t) && ri(h.n[0]) && ri(h.n[1]) && rd(h.x_start[1]) && rd(h.x_start[2]) && rd(h.dx[1]) &&
+              rd(h.dx[2]) && rd(h.t_final) && ri(h.n_step) && rd(h.a) && rd(h.gamma) && rd(h.courant) &&
+              rd(h.dt_dump) && rd(h.dt_log) && rd(h.dt_img) && ri(h.dt_rdump) && ri(h.cnt_dump) && ri(h.cnt_img) &&
+              ri(h.cnt_rdump) && rd(h.dt) && ri(h.lim) && ri(h.failed) && rd(h.r_in) && rd(h.r_out) &&
+              rd(h.h_slope) && rd(h.r_0);
+    if (!ok) {
+        std::fclose(fp);
+        return -2;
+    }
+    h.x_start[0] = 0.0;
+    h.x_start[3] = 0.0;
+    h.dx[0] = 1.0;
+    h.dx[3] = 2.0 * kPi;
+    h.x_stop[0] = 1.0;
+    h.x_stop[1] = h.x_start[1] + h.n[0] * h.dx[1];
+    h.x_stop[2] = h.x_start[2] + h.n[1] * h.dx[2];
+    h.x_stop[3] = 2.0 * kPi;
+    const double ttg = 0.5 * ((1. + 2. / 3. * (TP_OVER_TE + 1.) / (TP_OVER_TE + 2.)) + h.gamma);
+    m->units.theta_e_unit = (ttg - 1.) * (MP / ME) / (1. + TP_OVER_TE);
+    const size_t nz = (size_t)h.n[0] * h.n[1];
+    for (auto &f : m->fld) f.assign(nz, 0.0);
+    const double d_v = h.dx[1] * h.dx[2] * h.dx[3];
+    double v = 0.0, bn = 0.0;
+    for (size_t z = 0; z < nz; ++z) {
+        double tok[34];
+        for (int t = 0; t < 34; ++t)
+            if (std::fscanf(fp, "%lf", &tok[t]) != 1) {
+                std::fclose(fp);
+                return -3;
+            }
+        for (int f = 0; f < 8; ++f) m->fld[f][z] = tok[4 + f];
+        const double g_det = tok[33];
+        bn += d_v * g_det * std::pow(m->fld[1][z] / m->fld[0][z] * m->units.theta_e_unit, 2.);
+        v += d_v * g_det;
+    }
+    std::fclose(fp);
+    m->bias_norm = bn / v;
+    m->rh = 1.0 + std::sqrt(1.0 - h.a * h.a);
+    m->x1_min = std::log(m->rh);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* emission: harm_model.cpp:673-811, 1337-1389                                */
+/* ------------------------------------------------------------------------- */
+static void init_zone(const grmo_model *m, int x_1, int x_2, double &nz_o, double &dn_max_o) {
+    nz_o = 0.0;
+    dn_max_o = 0.0;
+    const Fluid fz = fluid_zone(m, x_1, x_2);
+    if (fz.n_e == 0.0 || fz.theta_e < THETA_E_MIN) return;
+    const double l_bth = std::log(fz.b * fz.theta_e * fz.theta_e);
+    double d_l = (l_bth - D.l_b_min) / (D.d_l_b);
+    const int l = (int)d_l;
+    d_l -= l;
+    if (l < 0) return;
+    double ninterp = 0.0, dn_max = 0.0;
+    if (l >= NINT) {
+        for (int i = 0; i <= N_E_SAMP; ++i) {
+            const double dn =
+                f_eval(m, fz.theta_e, fz.b, std::exp(x_2 * D.d_l_nu + D.l_nu_min)) / (std::exp(m->weight[i]) + 1.0e-100);
+            if (dn > dn_max) dn_max = dn;
+            ninterp += D.d_l_nu * dn;
+        }
+    } else if (!std::isinf(m->nint[l]) && !std::isinf(m->nint[l + 1])) {
+        ninterp = std::exp((1.0 - d_l) * m->nint[l] + d_l * m->nint[l + 1]);
+        dn_max = std::exp((1.0 - d_l) * m->dndlnu_max[l] + d_l * m->dndlnu_max[l + 1]);
+    }
+    const double k2 = k2_eval(m, fz.theta_e);
+    if (k2 == 0.0) return;
+    const double nz = m->det_z[(size_t)x_1 * m->n2() + x_2] * fz.n_e * fz.b * fz.theta_e * fz.theta_e * ninterp / k2;
+    if (nz > m->photon_n * std::log(NU_MAX / NU_MIN)) return;
+    nz_o = nz;
+    dn_max_o = dn_max;
+}
+
+static grmo_model::Zone get_zone(grmo_model *m, Rng &r) {
+    grmo_model::Zone z;
+    z.first_photon = true;
+    ++m->zone_x_2;
+    if (m->zone_x_2 >= m->n2()) {
+        m->zone_x_2 = 0;
+        ++m->zone_x_1;
+        if (m->zone_x_1 >= m->n1()) {
+            z.num_to_gen = 1;
+            z.x_1 = m->n1();
+            return z;
+        }
+    }
+    double d_num, dn_max;
+    init_zone(m, m->zone_x_1, m->zone_x_2, d_num, dn_max);
+    z.dn_max = dn_max;
+    int num;
+    if (std::fmod(d_num, 1.0) > r.uniform())
+        num = (int)d_num + 1;
+    else
+        num = (int)d_num;
+    z.x_1 = m->zone_x_1;
+    z.x_2 = m->zone_x_2;
+    z.num_to_gen = num;
+    return z;
+}
+
+static double linear_interp_weight(const grmo_model *m, double nu) { /* :784-792 */
+    const double l_nu = std::log(nu);
+    double d_i = (l_nu - D.l_nu_min) / D.d_l_nu;
+    const int i = (int)d_i;
+    d_i -= i;
+    return std::exp((1.0 - d_i) * m->weight[i] + d_i * m->weight[i + 1]);
+}
+
+static grmo_init_photon sample_zone_photon(grmo_model *m, grmo_model::Zone &zone, Rng &r) { /* :706-782 */
+    grmo_init_photon ph;
+    std::memset(&ph, 0, sizeof(ph));
+    coord_of(m, zone.x_1, zone.x_2, ph.x);
+    if (zone.first_photon) {
+        m->ez_fluid = fluid_zone(m, zone.x_1, zone.x_2);
+        double bh[4];
+        if (m->ez_fluid.b > 0.0) {
+            for (int i = 0; i < 4; ++i) bh[i] = m->ez_fluid.b_con[i] * m->units.b_unit / m->ez_fluid.b;
+        } else {
+            for (int i = 1; i < 4; ++i) bh[i] = 0.0;
+            bh[0] = 1.0;
+        }
+        double g[4][4];
+        std::memcpy(g, &m->gcov_z[((size_t)zone.x_1 * m->n2() + zone.x_2) * 16], sizeof(g));
+        make_tetrad(m->ez_fluid.u_con, bh, g, m->ez_econ, m->ez_ecov);
+        zone.first_photon = false;
+    }
+    const Fluid &fz = m->ez_fluid;
+    double nu, weight;
+    do {
+        nu = std::exp(r.uniform() * D.n_l_n + D.l_nu_min);
+        weight = linear_interp_weight(m, nu);
+    } while (r.uniform() > (f_eval(m, fz.theta_e, fz.b, nu) / (weight + 1.0e-100)) / zone.dn_max);
+    ph.w = weight;
+    const double j_max = synch(m, nu, fz.n_e, fz.theta_e, fz.b, kPi / 2.0);
+    double cos_th, th;
+    do {
+        cos_th = 2.0 * r.uniform() - 1.0;
+        th = std::acos(cos_th);
+    } while (r.uniform() > (synch(m, nu, fz.n_e, fz.theta_e, fz.b, th) / j_max));
+    const double sin_th = std::sqrt(1.0 - cos_th * cos_th);
+    const double phi = 2.0 * kPi * r.uniform();
+    const double cos_phi = std::cos(phi), sin_phi = std::sin(phi);
+    const double e = nu * HPL / (ME * CL * CL);
+    double kt[4] = {e, e * cos_th, e * sin_th * cos_phi, e * sin_th * sin_phi};
+    tetrad_to_coord(m->ez_econ, kt, ph.k);
+    kt[0] *= -1.0;
+    double tmp[4];
+    tetrad_to_coord(m->ez_ecov, kt, tmp);
+    ph.e = -tmp[0];
+    ph.e_0 = -tmp[0];
+    ph.l = tmp[3];
+    ph.n_e_0 = fz.n_e;
+    ph.theta_e_0 = fz.theta_e;
+    ph.b_0 = fz.b;
+    ph.n_scatt = 0;
+    return ph;
+}
+
+/* :794-811 */
+static bool make_super_photon(grmo_model *m, Rng &r, grmo_init_photon &out) {
+    while (m->zone.num_to_gen <= 0) m->zone = get_zone(m, r);
+    --m->zone.num_to_gen;
+    const bool quit = m->zone.x_1 == m->n1();
+    if (!quit) out = sample_zone_photon(m, m->zone, r);
+    return quit;
+}
+
+/* ========================================================================= */
+/* C ABI                                                                      */
+/* ========================================================================= */
+extern "C" {
+
+grmo_model *grmo_model_new(int photon_n, double mass_unit) {
+    grmo_model *m = new grmo_model();
+    m->photon_n = photon_n;
+    model_units(m, mass_unit);
+    return m;
+}
+
+void grmo_model_free(grmo_model *m) { delete m; }
+
+int grmo_model_read_file(grmo_model *m, const char *path) { return read_dump(m, path); }
+
+int grmo_model_set(grmo_model *m, const grmo_header *h, const double *const fields[8]) {
+    m->hdr = *h;
+    const double ttg = 0.5 * ((1. + 2. / 3. * (TP_OVER_TE + 1.) / (TP_OVER_TE + 2.)) + h->gamma);
+    m->units.theta_e_unit = (ttg - 1.) * (MP / ME) / (1. + TP_OVER_TE);
+    const size_t nz = (size_t)h->n[0] * h->n[1];
+    for (int f = 0; f < 8; ++f) m->fld[f].assign(fields[f], fields[f] + nz);
+    m->rh = 1.0 + std::sqrt(1.0 - h->a * h->a);
+    m->x1_min = std::log(m->rh);
+    m->bias_norm = 1.0;
+    return 0;
+}
+
+void grmo_model_get_header(const grmo_model *m, grmo_header *h) { *h = m->hdr; }
+void grmo_model_get_units(const grmo_model *m, grmo_units *u) { *u = m->units; }
+void grmo_model_get_scalars(const grmo_model *m, double out[5]) {
+    out[0] = m->bias_norm;
+    out[1] = m->rh;
+    out[2] = m->x1_min;
+    out[3] = m->max_tau_scatt;
+    out[4] = m->d_tau_k;
+}
+void grmo_model_set_max_tau_scatt(grmo_model *m, double v) { m->max_tau_scatt = v; }
+const double *grmo_model_field(const grmo_model *m, int which) { return m->fld[which].data(); }
+
+/* harm_model.cpp:242-266 */
+void grmo_init_geometry(grmo_model *m) {
+    const size_t nz = (size_t)m->n1() * m->n2();
+    m->gcov_z.assign(nz * 16, 0.0);
+    m->gcon_z.assign(nz * 16, 0.0);
+    m->det_z.assign(nz, 0.0);
+    for (int i = 0; i < m->n1(); ++i)
+        for (int j = 0; j < m->n2(); ++j) {
+            double x[4], gc[4][4], gn[4][4];
+            coord_of(m, i, j, x);
+            gcov_func(m, x, gc);
+            gcon_func(m, x, gn);
+            const size_t z = (size_t)i * m->n2() + j;
+            std::memcpy(&m->gcov_z[z * 16], gc, sizeof(gc));
+            std::memcpy(&m->gcon_z[z * 16], gn, sizeof(gn));
+            m->det_z[z] = std::sqrt(std::abs(det4(&m->gcov_z[z * 16])));
+        }
+}
+
+/* hotcross.cpp:60-79 */
+void grmo_init_hotcross(grmo_model *m, int n_threads) {
+    m->hotcross.assign((size_t)(HC_N_W + 1) * (HC_N_T + 1), 0.0);
+    if (n_threads < 1) n_threads = 1;
+    auto work = [m](int i0, int i1) {
+        for (int i = i0; i < i1; ++i)
+            for (int j = 0; j <= HC_N_T; ++j) {
+                const double l_w = D.hc_l_min_w + i * D.hc_d_l_w;
+                const double l_t = D.hc_l_min_t + j * D.hc_d_l_t;
+                m->hotcross[(size_t)i * (HC_N_T + 1) + j] = std::log10(hotcross_num(std::pow(10.0, l_w), std::pow(10.0, l_t)));
+            }
+    };
+    std::vector<std::thread> th;
+    const int rows = HC_N_W + 1;
+    for (int t = 0; t < n_threads; ++t) {
+        const int i0 = rows * t / n_threads, i1 = rows * (t + 1) / n_threads;
+        th.emplace_back(work, i0, i1);
+    }
+    for (auto &t : th) t.join();
+}
+
+/* jnu_mixed.cpp:57-73 */
+void grmo_init_emiss_tables(grmo_model *m) {
+    m->ftab.assign(N_E_SAMP + 1, 0.0);
+    m->k2.assign(N_E_SAMP + 1, 0.0);
+    for (int i = 0; i <= N_E_SAMP; ++i) {
+        const double k = std::exp(i * D.jnu_d_l_k + D.jnu_l_min_k);
+        const double res = gk61([k](double th) { return jnu_integrand(th, k); }, 0, kPi / 2.0, 0.0, 1.0e-6, 1000);
+        m->ftab[i] = std::log(4 * kPi * res);
+    }
+    for (int i = 0; i <= N_E_SAMP; ++i) {
+        const double t = std::exp(i * D.jnu_d_l_t + D.jnu_l_min_t);
+        m->k2[i] = std::log(std::cyl_bessel_k(2, 1.0 / t));
+    }
+}
+
+/* harm_model.cpp:268-306 */
+void grmo_init_weight_table(grmo_model *m) {
+    double sum[N_E_SAMP + 1], nu[N_E_SAMP + 1];
+    for (int i = 0; i <= N_E_SAMP; ++i) {
+        sum[i] = 0.0;
+        nu[i] = std::exp(i * D.d_l_nu + D.l_nu_min);
+    }
+    const Header &h = m->hdr;
+    const double s_fac = h.dx[1] * h.dx[2] * h.dx[3] * m->units.l_unit * m->units.l_unit * m->units.l_unit;
+    for (int i = 0; i < m->n1(); ++i)
+        for (int j = 0; j < m->n2(); ++j) {
+            const Fluid fz = fluid_zone(m, i, j);
+            if (fz.n_e == 0.0 || fz.theta_e < THETA_E_MIN) continue;
+            const double k2 = k2_eval(m, fz.theta_e);
+            const double fac =
+                (JCST * fz.n_e * fz.b * fz.theta_e * fz.theta_e / k2) * s_fac * m->det_z[(size_t)i * m->n2() + j];
+            for (int k = 0; k <= N_E_SAMP; ++k) sum[k] += fac * f_eval(m, fz.theta_e, fz.b, nu[k]);
+        }
+    m->weight.assign(N_E_SAMP + 1, 0.0);
+    for (int i = 0; i <= N_E_SAMP; ++i) m->weight[i] = std::log(sum[i] / (HPL * m->photon_n));
+}
+
+/* harm_model.cpp:308-338 */
+void grmo_init_nint_table(grmo_model *m) {
+    m->nint.assign(NINT + 1, 0.0);
+    m->dndlnu_max.assign(NINT + 1, 0.0);
+    const Header &h = m->hdr;
+    for (int i = 0; i <= NINT; ++i) {
+        double nint = 0.0, dmax = 0.0;
+        const double b_mag = std::exp(i * D.d_l_b + D.l_b_min);
+        for (int j = 0; j < N_E_SAMP; ++j) {
+            const double dn = f_eval(m, 1.0, b_mag, std::exp(j * D.d_l_nu + D.l_nu_min)) / (std::exp(m->weight[j]) + 1.0e-100);
+            if (dn > dmax) dmax = dn;
+            nint += D.d_l_nu * dn;
+        }
+        nint *= h.dx[1] * h.dx[2] * h.dx[3] * m->units.l_unit * m->units.l_unit * m->units.l_unit * kSqrt2 * EE * EE *
+                EE / (27.0 * ME * CL * CL) * (1.0 / HPL);
+        m->nint[i] = std::log(nint);
+        m->dndlnu_max[i] = std::log(dmax);
+    }
+}
+
+void grmo_init_all(grmo_model *m, int n_threads) {
+    grmo_init_geometry(m);
+    grmo_init_hotcross(m, n_threads);
+    grmo_init_emiss_tables(m);
+    grmo_init_weight_table(m);
+    grmo_init_nint_table(m);
+}
+
+const double *grmo_table(const grmo_model *m, int which) {
+    switch (which) {
+    case 0: return m->hotcross.data();
+    case 1: return m->k2.data();
+    case 2: return m->ftab.data();
+    case 3: return m->weight.data();
+    case 4: return m->nint.data();
+    case 5: return m->dndlnu_max.data();
+    case 6: return m->det_z.data();
+    default: return nullptr;
+    }
+}
+
+void grmo_set_table(grmo_model *m, int which, const double *src) {
+    switch (which) {
+    case 0: m->hotcross.assign(src, src + (size_t)(HC_N_W + 1) * (HC_N_T + 1)); break;
+    case 1: m->k2.assign(src, src + N_E_SAMP + 1); break;
+    case 2: m->ftab.assign(src, src + N_E_SAMP + 1); break;
+    case 3: m->weight.assign(src, src + N_E_SAMP + 1); break;
+    case 4: m->nint.assign(src, src + NINT + 1); break;
+    case 5: m->dndlnu_max.assign(src, src + NINT + 1); break;
+    default: break;
+    }
+}
+
+void grmo_gcov(const grmo_model *m, const double x[4], double g[16]) {
+    double t[4][4];
+    gcov_func(m, x, t);
+    std::memcpy(g, t, sizeof(t));
+}
+void grmo_gcon(const grmo_model *m, const double x[4], double g[16]) {
+    double t[4][4];
+    gcon_func(m, x, t);
+    std::memcpy(g, t, sizeof(t));
+}
+void grmo_connection(const grmo_model *m, const double x[4], double lconn[64]) {
+    double L[4][4][4];
+    std::memset(L, 0, sizeof(L));
+    get_connection(m, x, L);
+    std::memcpy(lconn, L, sizeof(L));
+}
+void grmo_init_dkdlam(const grmo_model *m, const double x[4], const double k[4], double dk[4]) {
+    init_dkdlam(m, x, k, dk);
+}
+double grmo_step_size(const grmo_model *m, const double x[4], const double k[4]) { return step_size(m, x, k); }
+void grmo_push_photon(const grmo_model *m, double s[13], double dl) {
+    push_photon(m, s, s + 4, s + 8, s[12], dl, 0);
+}
+void grmo_fluid_params(const grmo_model *m, const double x[4], grmo_fluid *out) {
+    double g[4][4];
+    gcov_func(m, x, g);
+    fluid_params(m, x, g, *out);
+}
+double grmo_bk_angle(const double k[4], const grmo_fluid *f, double b_unit) {
+    return bk_angle(k, f->u_cov, f->b_cov, f->b, b_unit);
+}
+double grmo_fluid_nu(const double k[4], const double u_cov[4]) { return fluid_nu(k, u_cov); }
+double grmo_alpha_inv_scatt(const grmo_model *m, double nu, double theta_e, double n_e) {
+    return alpha_inv_scatt(m, nu, theta_e, n_e);
+}
+double grmo_alpha_inv_abs(const grmo_model *m, double nu, double theta_e, double n_e, double b, double theta) {
+    return alpha_inv_abs(m, nu, theta_e, n_e, b, theta);
+}
+double grmo_hotcross_lookup(const grmo_model *m, double w, double theta_e) { return hotcross_lkup(m, w, theta_e); }
+double grmo_hotcross_num(double w, double theta_e) { return hotcross_num(w, theta_e); }
+double grmo_synch(const grmo_model *m, double nu, double n_e, double theta_e, double b, double theta) {
+    return synch(m, nu, n_e, theta_e, b, theta);
+}
+double grmo_k2_eval(const grmo_model *m, double theta_e) { return k2_eval(m, theta_e); }
+double grmo_f_eval(const grmo_model *m, double theta_e, double b, double nu) { return f_eval(m, theta_e, b, nu); }
+void grmo_make_tetrad(const double u_con[4], const double trial[4], const double g_cov[16], double e_con[16],
+                      double e_cov[16]) {
+    double g[4][4], ec[4][4], el[4][4], tr[4];
+    std::memcpy(g, g_cov, sizeof(g));
+    std::memcpy(tr, trial, sizeof(tr));
+    make_tetrad(u_con, tr, g, ec, el);
+    std::memcpy(e_con, ec, sizeof(ec));
+    std::memcpy(e_cov, el, sizeof(el));
+}
+void grmo_boost(const double v[4], const double u[4], double vp[4]) { boost(v, u, vp); }
+
+/* known-answer integrands for GK61 (tests/integration_test.cpp-style) */
+double grmo_gk61(int which, double param, double a, double b, double eps_abs, double eps_rel, int max_iv) {
+    std::function<double(double)> f;
+    switch (which) { /* the integrands of the reference's tests/integration_test.cpp:18-116, then jnu */
+    case 0: f = [](double) { return 1.0; }; break;
+    case 1: f = [](double x) { return 2.0 * x + 1.0; }; break;
+    case 2: f = [](double x) { return -x * x + 1.0; }; break;
+    case 3: f = [](double x) { return std::sin(x); }; break;
+    case 4: f = [](double x) { return std::abs(x - 0.3); }; break;
+    case 5: f = [](double x) { return std::sqrt(x); }; break;
+    case 6: f = [](double x) { return std::log(x); }; break;
+    case 7: f = [](double x) { return std::sin(20 * x); }; break;
+    case 8: f = [](double x) { return 1.0 / (1.0 + 1000.0 * (x - 0.5) * (x - 0.5)); }; break;
+    case 9: f = [](double x) { return (x < 0.5) ? 0.0 : 1.0; }; break;
+    case 10: f = [param](double th) { return jnu_integrand(th, param); }; break;
+    default: f = [](double x) { return x; }; break;
+    }
+    try {
+        return gk61(f, a, b, eps_abs, eps_rel, max_iv);
+    } catch (...) {
+        return std::nan("");
+    }
+}
+
+struct grmo_rng {
+    Rng r;
+    std::mt19937 mt;
+};
+
+grmo_rng *grmo_rng_new(int mode, uint64_t seed, uint64_t id) {
+    grmo_rng *g = new grmo_rng();
+    if (mode == GRMO_RNG_MT19937) {
+        g->mt = std::mt19937((std::mt19937::result_type)seed);
+        g->r.mode = GRMO_RNG_MT19937;
+        g->r.mt = &g->mt;
+    } else {
+        g->r = Rng::philox(seed, id);
+    }
+    return g;
+}
+void grmo_rng_free(grmo_rng *r) { delete r; }
+double grmo_rng_uniform(grmo_rng *r) { return r->r.uniform(); }
+double grmo_rng_chi_sq(grmo_rng *r, int dof) { return r->r.chi_sq(dof); }
+uint64_t grmo_rng_counter(const grmo_rng *r) { return r->r.ctr; }
+void grmo_sample_electron(grmo_rng *r, const double k[4], double p[4], double theta_e) {
+    sample_electron(r->r, k, p, theta_e);
+}
+double grmo_sample_klein_nishina(grmo_rng *r, double k0) { return sample_klein_nishina(r->r, k0); }
+double grmo_sample_thomson(grmo_rng *r) { return sample_thomson(r->r); }
+void grmo_sample_rand_dir(grmo_rng *r, double out[3]) { sample_rand_dir(r->r, out[0], out[1], out[2]); }
+void grmo_sample_scattered(grmo_rng *r, const double k[4], const double p_in[4], double kp[4]) {
+    double p[4] = {p_in[0], p_in[1], p_in[2], p_in[3]};
+    sample_scattered(r->r, k, p, kp);
+}
+void grmo_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { philox4x32_10(ctr, key, out); }
+uint64_t grmo_child_id(uint64_t parent_id, uint64_t parent_ctr) { return child_id(parent_id, parent_ctr); }
+
+int64_t grmo_track_batch(grmo_model *m, const grmo_init_photon *ph, size_t n, int rng_mode, uint64_t seed,
+                         uint64_t id_base, int bias_mode, uint64_t scatt0, uint64_t rec0, double max_tau0,
+                         grmo_trace *trace, size_t trace_cap) {
+    m->bias_mode = bias_mode;
+    m->b_scatt0 = scatt0;
+    m->b_rec0 = rec0;
+    m->b_maxtau0 = max_tau0;
+    m->trace = trace;
+    m->trace_cap = trace ? trace_cap : 0;
+    m->trace_n = 0;
+    std::mt19937 mt((std::mt19937::result_type)seed);
+    TrackCtx C{m, rng_mode, seed, &mt};
+    Rng shared;
+    shared.mode = GRMO_RNG_MT19937;
+    shared.mt = &mt;
+    for (size_t i = 0; i < n; ++i) {
+        Photon p = from_init(ph[i]);
+        p.id = id_base + i;
+        p.parent_id = ~0ull;
+        if (rng_mode == GRMO_RNG_PHILOX) {
+            Rng r = Rng::philox(seed, p.id);
+            track_super_photon(C, p, r);
+        } else {
+            track_super_photon(C, p, shared);
+        }
+        ++m->n_created;
+    }
+    m->trace = nullptr;
+    m->bias_mode = GRMO_BIAS_LIVE;
+    return m->trace_n;
+}
+
+void grmo_reset_spectrum(grmo_model *m) {
+    std::memset(m->spectrum, 0, sizeof(m->spectrum));
+    m->n_created = m->n_scatt = m->n_recorded = m->n_steps = 0;
+}
+
+void grmo_get_spectrum(const grmo_model *m, grmo_spectrum out[6 * 200]) {
+    std::memcpy(out, m->spectrum, sizeof(m->spectrum));
+}
+
+void grmo_get_counters(const grmo_model *m, uint64_t out[4]) {
+    out[0] = m->n_created;
+    out[1] = m->n_scatt;
+    out[2] = m->n_recorded;
+    out[3] = m->n_steps;
+}
+
+int64_t grmo_emit(grmo_model *m, uint64_t seed, grmo_init_photon *out, size_t cap, int *done) {
+    /* the zone walk and its mt19937 stream live in the model (harm_model.cpp:795 static Zone) */
+    if (!m->emit_started || m->emit_seed != seed) {
+        m->emit_mt = std::mt19937((std::mt19937::result_type)seed);
+        m->emit_seed = seed;
+        m->emit_started = true;
+    }
+    Rng r;
+    r.mode = GRMO_RNG_MT19937;
+    r.mt = &m->emit_mt;
+    size_t k = 0;
+    *done = 0;
+    while (k < cap) {
+        grmo_init_photon ip;
+        if (make_super_photon(m, r, ip)) {
+            *done = 1;
+            break;
+        }
+        out[k++] = ip;
+    }
+    return (int64_t)k;
+}
+
+void grmo_init_zone(const grmo_model *m, int i, int j, double out[2]) { init_zone(m, i, j, out[0], out[1]); }
+
+/* harm_model.cpp:340-414 (CPU branch) */
+double grmo_run_simulation(grmo_model *m, uint64_t seed) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::mt19937 mt((std::mt19937::result_type)seed);
+    Rng r;
+    r.mode = GRMO_RNG_MT19937;
+    r.mt = &mt;
+    TrackCtx C{m, GRMO_RNG_MT19937, seed, &mt};
+    m->bias_mode = GRMO_BIAS_LIVE;
+    while (true) {
+        grmo_init_photon ip;
+        if (make_super_photon(m, r, ip)) break;
+        Photon p = from_init(ip);
+        track_super_photon(C, p, r);
+        ++m->n_created;
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+/* harm_model.cpp:416-471, 532-536 */
+int grmo_report_spectrum(const grmo_model *m, const char *path, double out[2]) {
+    const Header &h = m->hdr;
+    const double dx2 = (h.x_stop[2] - h.x_start[2]) / (2 * N_TH_BINS);
+    auto d_omega = [&](double x2i, double x2f) {
+        return 2.0 * kPi *
+               (-std::cos(kPi * x2f + 0.5 * (1.0 - h.h_slope) * std::sin(2 * kPi * x2f)) +
+                std::cos(kPi * x2i + 0.5 * (1.0 - h.h_slope) * std::sin(2 * kPi * x2i)));
+    };
+    FILE *fp = path ? std::fopen(path, "w") : nullptr;
+    if (path && !fp) return -1;
+    double maxt = 0.0, lum = 0.0;
+    for (int i = 0; i < N_E_BINS; ++i) {
+        if (fp) std::fprintf(fp, "%10.5g ", (i * SPEC_D_L_E + D.spec_l_e_0) / kLn10);
+        for (int j = 0; j < N_TH_BINS; ++j) {
+            const grmo_spectrum &s = m->spectrum[j][i];
+            const double dom = 2.0 * d_omega(j * dx2, (j + 1) * dx2);
+            double nu_lnu = (ME * CL * CL) * (4.0 * kPi / dom) * (1.0 / SPEC_D_L_E);
+            nu_lnu *= s.de_dle;
+            nu_lnu /= L_SUN;
+            const double ts = s.tau_scatt / (s.dn_dle + EPS);
+            if (fp) {
+                std::fprintf(fp, "%10.5g ", nu_lnu);
+                std::fprintf(fp, "%10.5g ", s.tau_abs / (s.dn_dle + EPS));
+                std::fprintf(fp, "%10.5g ", ts);
+                std::fprintf(fp, "%10.5g ", s.x1i_av / (s.dn_dle + EPS));
+                std::fprintf(fp, "%10.5g ", std::sqrt(std::abs(s.x2i_sq / (s.dn_dle + EPS))));
+                std::fprintf(fp, "%10.5g ", std::sqrt(std::abs(s.x3f_sq / (s.dn_dle + EPS))));
+            }
+            if (ts > maxt) maxt = ts;
+            lum += nu_lnu * dom * SPEC_D_L_E;
+        }
+        if (fp) std::fprintf(fp, "\n");
+    }
+    if (fp) std::fclose(fp);
+    if (out) {
+        out[0] = lum;
+        out[1] = maxt;
+    }
+    return 0;
+}
+
+size_t grmo_sizeof(int which) {
+    switch (which) {
+    case 0: return sizeof(grmo_header);
+    case 1: return sizeof(grmo_units);
+    case 2: return sizeof(grmo_init_photon);
+    case 3: return sizeof(grmo_spectrum);
+    case 4: return sizeof(grmo_fluid);
+    case 5: return sizeof(grmo_trace);
+    default: return 0;
+    }
+}
+
+} /* extern "C" */
+extern "C" void grmo_dbg_push_stats(uint64_t out[3]) {
+    out[0] = g_dbg_attempts;
+    out[1] = g_dbg_iter2;
+    out[2] = g_dbg_fail;
+}
+extern "C" double grmo_dbg_sample_y(grmo_rng *r, double t) { return sample_y_distr(r->r, t); }
+extern "C" double grmo_dbg_sample_mu(grmo_rng *r, double b) { return sample_mu_distr(r->r, b); }

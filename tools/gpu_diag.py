@@ -1,0 +1,36 @@
+"""Quick GPU performance snapshot: transport of an emitted batch, kernel time, steps/s."""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "cuda-grmonty_amd"))
+import numpy as np  # noqa: E402
+
+import grmonty_amd as G  # noqa: E402
+from grmonty_amd.synth_dump import ensure_dump  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 192
+photon_n = int(float(sys.argv[2])) if len(sys.argv) > 2 else 100000
+grid = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+path = ensure_dump(os.path.join(REPO, "gpurun_out", f"synth{n}.dump"), n, n)
+t = time.time()
+m = G.Model.load(path, photon_n=photon_n).init(0)
+print(f"init {time.time() - t:.2f}s", flush=True)
+t = time.time()
+ph = m.emit(seed=123)
+print(f"emit {len(ph)} photons {time.time() - t:.2f}s", flush=True)
+e = G.Engine(m, 0)
+if grid:
+    e.set_option(G.OPT_GRID_BLOCKS, grid)
+for rep in range(3):
+    e.reset()
+    t = time.time()
+    e.track(ph)
+    wall = time.time() - t
+    spec, nr, ns, mt = e.finish()
+    st = e.stats()
+    print(f"rep {rep}: wall {wall:.3f}s kernel {st['last_kernel_ms']:.1f}ms steps {st['last_steps']} "
+          f"({st['last_steps'] / st['last_kernel_ms'] / 1e3:.3g} Msteps/s) tracked {st['n_tracked']} "
+          f"children {st['n_children']} overflow {st['n_overflow']} launches {st['n_launches']} "
+          f"rate {len(ph) / (st['last_kernel_ms'] * 1e-3):.4g} ph/s rec {nr} scatt {ns}", flush=True)
