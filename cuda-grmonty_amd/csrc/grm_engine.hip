@@ -29,14 +29,19 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "grm_device.h"
 
 using namespace grm;
 
 namespace {
 
+#ifndef GRM_WAVES_PER_SIMD
+#define GRM_WAVES_PER_SIMD 1
+#endif
 constexpr int BLOCK = 256;
-constexpr int MIN_WAVES_PER_SIMD = 2;
+constexpr int MIN_WAVES_PER_SIMD = GRM_WAVES_PER_SIMD;
 constexpr int STACK_DEPTH = 8;
 
 /* 208-B scatter request: the state at a scattering event from which the child
@@ -631,6 +636,9 @@ struct grm_engine {
     uint64_t history = 0;    /* primaries tracked since reset */
     double fz_scatt = 0.0, fz_rec = 0.0, fz_maxtau = 0.0;
     grm_stats stats{};
+    grm_init_photon *d_upload = nullptr;
+    size_t upload_cap = 0;
+    ncclComm_t comm = nullptr;
     std::string err;
 };
 
@@ -884,6 +892,8 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_small);
     hipFree(e->d_batch);
     hipFree(e->d_trace);
+    hipFree(e->d_upload);
+    if (e->comm) ncclCommDestroy(e->comm);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
     if (e->stream) hipStreamDestroy(e->stream);
@@ -988,6 +998,68 @@ int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap) {
     const size_t k = std::min(avail, cap);
     if (k && out && hipMemcpy(out, e->d_trace, k * sizeof(grm_trace), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     return (int64_t)cnt;
+}
+
+int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm_init_photon **dev_out) {
+    if (!e || !dev_out || (!batch && n)) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (n > e->upload_cap) {
+        if (e->d_upload) (void)hipFree(e->d_upload);
+        e->d_upload = nullptr;
+        e->upload_cap = 0;
+        HIPCHK(e, hipMalloc(&e->d_upload, n * sizeof(grm_init_photon)));
+        e->upload_cap = n;
+    }
+    HIPCHK(e, hipMemcpy(e->d_upload, batch, n * sizeof(grm_init_photon), hipMemcpyHostToDevice));
+    *dev_out = e->d_upload;
+    return 0;
+}
+
+int grm_rccl_unique_id(uint8_t id_out[128]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+    std::memcpy(id_out, &id, sizeof(id));
+    return 0;
+}
+
+int grm_engine_comm_init(grm_engine *e, const uint8_t id_in[128], int nranks, int rank) {
+    if (!e || !id_in) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id_in, sizeof(id));
+    const ncclResult_t r = ncclCommInitRank(&e->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        e->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+        e->comm = nullptr;
+        return -1;
+    }
+    return 0;
+}
+
+int grm_engine_allreduce(grm_engine *e) {
+    if (!e) return -1;
+    if (!e->comm) {
+        e->err = "grm_engine_allreduce: no communicator (grm_engine_comm_init)";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    const size_t ncell = (size_t)N_TH_BINS * N_E_BINS * (sizeof(grm_spectrum_cell) / sizeof(double));
+    unsigned long long *c = reinterpret_cast<unsigned long long *>(e->d_ctr);
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) r = ncclAllReduce(e->d_spec, e->d_spec, ncell, ncclFloat64, ncclSum, e->comm, e->stream);
+    /* DevCounters: [0..1] n_recorded n_scatt (sum), [2] max_tau bits (max; tau >= 0 orders as u64),
+     * [3..8] steps/tracked/children/overflow/dropped/primaries (sum) */
+    if (r == ncclSuccess) r = ncclAllReduce(c, c, 2, ncclUint64, ncclSum, e->comm, e->stream);
+    if (r == ncclSuccess) r = ncclAllReduce(c + 2, c + 2, 1, ncclUint64, ncclMax, e->comm, e->stream);
+    if (r == ncclSuccess) r = ncclAllReduce(c + 3, c + 3, 6, ncclUint64, ncclSum, e->comm, e->stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess) {
+        e->err = std::string("RCCL all-reduce: ") + ncclGetErrorString(r);
+        return -1;
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return 0;
 }
 
 int grm_probe(grm_engine *e, int which, const double *in, int in_stride, double *out, int out_stride, size_t n) {

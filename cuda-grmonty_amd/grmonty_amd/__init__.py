@@ -20,7 +20,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libgrmonty_amd.so")
+LIB_PATH = os.environ.get("GRMONTY_AMD_LIB") or os.path.join(PKG_DIR, "libgrmonty_amd.so")
 REPO_DIR = os.path.dirname(PKG_DIR)
 HEADER_PATH = os.path.join(REPO_DIR, "include", "grmonty_amd.h")
 
@@ -93,6 +93,10 @@ SIGNATURES = {
     "grm_model_zone_weights": (C.c_int, [VP, DP]),
     "grm_write_spectrum": (C.c_int, [VP, VP, C.c_char_p, DP]),
     "grm_probe": (C.c_int, [VP, C.c_int, DP, C.c_int, DP, C.c_int, C.c_size_t]),
+    "grm_engine_upload": (C.c_int, [VP, VP, C.c_size_t, C.POINTER(VP)]),
+    "grm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "grm_engine_comm_init": (C.c_int, [VP, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    "grm_engine_allreduce": (C.c_int, [VP]),
     "grm_sizeof": (C.c_size_t, [C.c_int]),
     "grm_version": (C.c_char_p, []),
 }
@@ -274,6 +278,20 @@ class Engine:
             raise RuntimeError("trace not enabled")
         return out[:min(n, cap)]
 
+    def upload(self, photons: np.ndarray) -> int:
+        """Copy photons into an engine-owned device buffer; returns its device address."""
+        ph = np.ascontiguousarray(photons, dtype=INIT_PHOTON)
+        out = VP()
+        self._check(self.L.grm_engine_upload(self.h, _ptr(ph), len(ph), C.byref(out)))
+        return int(out.value or 0)
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.L.grm_engine_comm_init(self.h, buf, nranks, rank))
+
+    def allreduce(self):
+        self._check(self.L.grm_engine_allreduce(self.h))
+
     def probe(self, which: int, inputs: np.ndarray, out_width: int) -> np.ndarray:
         a = np.ascontiguousarray(inputs, dtype=np.float64)
         if a.ndim == 1:
@@ -282,6 +300,29 @@ class Engine:
         self._check(self.L.grm_probe(self.h, which, a.ctypes.data_as(DP), a.shape[1], out.ctypes.data_as(DP),
                                      out_width, a.shape[0]))
         return out
+
+
+def shard_zones(zone_weights: np.ndarray, world: int) -> list[tuple[int, int]]:
+    """Contiguous zone ranges [z0, z1) with ~equal expected photon counts (init_zone's nz,
+    harm_model.cpp:1337-1389) -- the multi-GPU partition of one run.  Zone streams are keyed by
+    zone index, so the union over ranks emits exactly the single-GPU photon list."""
+    w = np.asarray(zone_weights, dtype=np.float64)
+    c = np.cumsum(w)
+    tot = c[-1] if len(c) else 0.0
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(c, tot * r / world, side="right")))
+    cuts.append(len(w))
+    for r in range(1, len(cuts)):
+        cuts[r] = max(cuts[r], cuts[r - 1])
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def rccl_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    if lib().grm_rccl_unique_id(buf) != 0:
+        raise RuntimeError("ncclGetUniqueId failed")
+    return bytes(buf)
 
 
 def header_symbols(path: str = HEADER_PATH) -> list[str]:

@@ -158,6 +158,17 @@ int grm_engine_stats(const grm_engine *e, grm_stats *out);
 void *grm_engine_spectrum_device_ptr(grm_engine *e);
 /* copy the per-photon trace (requires GRM_OPT_TRACE_CAP > 0); returns records produced. */
 int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap);
+/* copy a host batch into an engine-owned device buffer once (inputs resident in HBM); *dev_out is
+ * valid for grm_engine_track_device until the next upload or destroy. */
+int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm_init_photon **dev_out);
+
+/* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
+/* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */
+int grm_rccl_unique_id(uint8_t id_out[128]);
+int grm_engine_comm_init(grm_engine *e, const uint8_t id[128], int nranks, int rank);
+/* in-place all-reduce of the spectrum (fp64 sum), counters (u64 sum) and max tau_scatt (max):
+ * the only exchange step of the path (photon shards are independent). */
+int grm_engine_allreduce(grm_engine *e);
 
 /* --- host model (harm_model.hpp; C++ host, no GPU) ------------------------------------- */
 typedef struct grm_model grm_model;
