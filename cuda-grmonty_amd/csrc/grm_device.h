@@ -285,7 +285,7 @@ __device__ __forceinline__ double step_size(const Params &P, const double x[4], 
 /* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
  * predicate of :1279 and the new energy e_1; leaves Gcov at the new x in G. */
 __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
-                                             double dl, double &e_1, Gcov &G) {
+                                             double dl, double &e_1, Trig &T, Gcov &G) {
     const double dl_2 = 0.5 * dl;
     double kp[4];
 #pragma unroll
@@ -295,7 +295,6 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
         kp[i] = k[i] + d;
         x[i] += k[i] * dl;
     }
-    Trig T;
     trig_at(P, x, T);
     Conn C;
     connection(P, T, C);
@@ -346,8 +345,9 @@ __device__ __forceinline__ void push_photon(const Params &P, double x[4], double
                 bk[8 + i] = dk[i];
             }
             double e_1;
+            Trig T;
             Gcov G;
-            const bool fail = push_attempt(P, x, k, dk, e_0_s, ldexp(dl, -depth), e_1, G);
+            const bool fail = push_attempt(P, x, k, dk, e_0_s, ldexp(dl, -depth), e_1, T, G);
             if (fail && depth < MAX_SUBDIV) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {

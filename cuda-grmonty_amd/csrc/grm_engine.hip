@@ -42,7 +42,8 @@ namespace {
 #endif
 constexpr int BLOCK = 256;
 constexpr int MIN_WAVES_PER_SIMD = GRM_WAVES_PER_SIMD;
-constexpr int STACK_DEPTH = 8;
+constexpr int STACK_DEPTH = 8;                  /* scatter-request slots per lane ... */
+constexpr int WSTACK_CAP = 64 * STACK_DEPTH;    /* ... pooled into one stack per wave */
 
 /* 208-B scatter request: the state at a scattering event from which the child
  * photon is sampled later (scatter_super_photon, harm_model.cpp:1071-1145).
@@ -92,6 +93,8 @@ struct Ctl {
     unsigned long long *trace_count;
     int bias_frozen;
     double f_scatt, f_rec, f_maxtau;
+    unsigned long long *timing; /* GRM_TIMING builds: per-region wave cycles */
+    int refill_min;             /* idle lanes a wave gathers before it refills (batching) */
 };
 
 /* hot photon state: lives in VGPRs for the photon's whole life */
@@ -101,27 +104,69 @@ struct Lane {
     double alpha_scatti, alpha_absi, bi, fl_ne;
     int n_scatt, n_step;
     Rng rng;
+    /* per-trip push state machine: phase 0 = loop top, 1 = geodesic step in progress,
+     * 2 = re-push to the scattering point in progress; depth/pend = position in the halving tree */
+    int phase, depth;
+    uint32_t pend;
+    double dl, hlen;                      /* step size of this iteration; length being pushed */
+    double p_dtau_abs, p_dtau_scatt, p_wc; /* carried across the re-push */
 };
 
-__device__ __forceinline__ double bias_func(const Params &P, const Ctl &C, double t_e, double w) {
+/* Denominator of bias_func's first term, bias_norm * max_tau_scatt * (<N_scatt> + 2)
+ * (harm_model.cpp:1391-1404).  Wave-uniform: computed once per refresh at a converged point of the
+ * lane loop from the frozen snapshot or from the live device counters -- the live counters sit in
+ * device-coherent memory (every XCD adds to them), so loading them per step would put a
+ * cross-die round trip on every interaction. */
+__device__ __forceinline__ double bias_den(const Params &P, const Ctl &C) {
     double scatt, rec, mts;
     if (C.bias_frozen) {
         scatt = C.f_scatt;
         rec = C.f_rec;
         mts = C.f_maxtau;
-    } else { /* live, reference-like adaptive bias (harm_model.cpp:1391-1404) */
+    } else { /* live, reference-like adaptive bias */
         scatt = (double)__hip_atomic_load(&C.ctr->n_scatt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rec = (double)__hip_atomic_load(&C.ctr->n_recorded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         mts = __longlong_as_double(
             (long long)__hip_atomic_load(&C.ctr->max_tau_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
-    const double max = 0.5 * w / WEIGHT_MIN;
     const double avg = scatt / (1.0 * rec + 1.0);
-    double bias = 100.0 * t_e * t_e / (P.bias_norm * mts * (avg + 2.0));
+    const long long d = __double_as_longlong(P.bias_norm * mts * (avg + 2.0));
+    const int lo = __builtin_amdgcn_readfirstlane((int)(d & 0xffffffffll));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(d >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+/* bias_func (harm_model.cpp:1391-1404), same expression and rounding as the reference */
+__device__ __forceinline__ double bias_func(double den, double t_e, double w) {
+    const double max = 0.5 * w / WEIGHT_MIN;
+    double bias = 100.0 * t_e * t_e / den;
     if (bias < TP_OVER_TE) bias = TP_OVER_TE;
     if (bias > max) bias = max;
     return bias / TP_OVER_TE;
 }
+
+/* Diagnostic build (-DGRM_TIMING): per-wave cycle attribution with s_memtime stamps, accumulated in
+ * LDS by the first active lane.  Slots: 0 child refill+sampling, 1 pool refill+init, 2 transport
+ * trip, 3 loop total, 4 trips, 5 trips with a child sampled, 6 trips with an init, 7 bias refresh,
+ * 8 phase-0 block, 9 push attempt, 10 restore / halving bookkeeping, 11 fluid gather,
+ * 12 radiation + bias, 13 rest of the interaction; 15 = last stamp.  Never built into the product. */
+#ifdef GRM_TIMING
+__shared__ unsigned long long g_tlds[4][16];
+__device__ __forceinline__ void tstamp(int r) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    const unsigned long long ex = __ballot(1);
+    const int w = threadIdx.x >> 6;
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)ex) - 1) {
+        g_tlds[w][r] += t - g_tlds[w][15];
+        g_tlds[w][15] = t;
+    }
+}
+#define TSTAMP(r) tstamp(r)
+#define TCOUNT(r) do { if ((threadIdx.x & 63) == 0) g_tlds[threadIdx.x >> 6][r] += 1; } while (0)
+#else
+#define TSTAMP(r) do { } while (0)
+#define TCOUNT(r) do { } while (0)
+#endif
 
 /* stop_criterion (harm_model.cpp:1589-1616) */
 __device__ __forceinline__ bool stop_criterion(const Params &P, Lane &L) {
@@ -227,7 +272,7 @@ __device__ __forceinline__ void end_of_life(const Params &P, const Ctl &C, const
 }
 
 /* photon set-up at the head of track_super_photon (harm_model.cpp:895-917). false = invalid */
-__device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lane &L) {
+__device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lane &L, double bias_d) {
     if (isnan(L.x[0]) || isnan(L.x[1]) || isnan(L.x[2]) || isnan(L.x[3]) || isnan(L.k[0]) || isnan(L.k[1]) ||
         isnan(L.k[2]) || isnan(L.k[3]) || L.w == 0.0) {
         trace_end(C, cold, L, 4);
@@ -243,7 +288,7 @@ __device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lan
     const double nu = fluid_nu(L.k, F);
     L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
     L.alpha_absi = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
-    L.bi = bias_func(P, C, F.theta_e, L.w);
+    L.bi = bias_func(bias_d, F.theta_e, L.w);
     L.fl_ne = F.n_e;
     Conn Cn;
     connection(P, T, Cn);
@@ -252,6 +297,7 @@ __device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lan
     L.n_step = 0;
     L.tau_abs = L.tau_scatt = 0.0;
     L.e_0_s = cold->e;
+    L.phase = 0;
     return true;
 }
 
@@ -364,141 +410,209 @@ __device__ __forceinline__ void store_sreq(SReq *dst, const SReq &R) {
     for (int q = 0; q < 13; ++q) d[q] = s[q];
 }
 
-/* one iteration of the while loop of track_super_photon (harm_model.cpp:919-1063).
- * returns false when the photon's life ended. */
-__device__ bool transport_step(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *my_stack, int &sdepth,
-                               unsigned long long &steps, const Slot &ph2, const Slot &bk) {
-    if (stop_criterion(P, L)) {
-        end_of_life(P, C, cold, L);
-        return false;
-    }
-    /* photon_2 (harm_model.cpp:920-925): only read back if this step scatters -> LDS */
+/* push the scattered photon's child out as a scatter request: onto the wave's stack (HBM entries,
+ * top counter in LDS), else the overflow pool */
+__device__ __forceinline__ void push_request(const Ctl &C, const Lane &L, const Cold *cold, const Fluid &F, double wc,
+                                             SReq *wstack, int *wtop) {
+    SReq R;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        ph2[i] = L.x[i];
-        ph2[4 + i] = L.k[i];
-        ph2[8 + i] = L.dk[i];
+        R.x[i] = L.x[i];
+        R.k[i] = L.k[i];
+        R.u_con[i] = F.u_con[i];
+        R.b_con[i] = F.b_con[i];
     }
-    ph2[12] = L.e_0_s;
-    const double dl = step_size(P, L.x, L.k);
-    push_photon(P, L.x, L.k, L.dk, L.e_0_s, dl, bk);
-    ++steps;
-    if (stop_criterion(P, L)) {
-        end_of_life(P, C, cold, L);
-        return false;
+    R.b = F.b;
+    R.theta_e = F.theta_e;
+    R.w = wc;
+    R.n_e_0 = cold->n_e_0;
+    R.theta_e_0 = cold->theta_e_0;
+    R.e_0 = cold->e_0;
+    R.id = child_id(L.rng.id, L.rng.ctr);
+    R.parent = L.rng.id;
+    R.n_scatt = L.n_scatt + 1;
+    R.pad0 = 0;
+    R.pad1 = 0.0;
+    const int slot = atomicAdd(wtop, 1); /* LDS; values past the cap are clamped at the next refill */
+    if (slot < WSTACK_CAP) {
+        store_sreq(wstack + slot, R);
+    } else {
+        const unsigned long long o = atomicAdd(C.ovf_count, 1ull);
+        if (o < C.ovf_cap)
+            store_sreq(C.ovf + o, R);
+        else
+            atomicAdd(&C.ctr->n_dropped, 1ull);
+        atomicAdd(&C.ctr->n_overflow, 1ull);
     }
-    if (L.alpha_absi > 0.0 || L.alpha_scatti > 0.0 || L.fl_ne > 0.0) {
-        Trig T;
-        trig_at(P, L.x, T);
-        Gcov G;
-        gcov_from_trig(P, T, G);
-        Fluid F;
-        fluid_params(P, L.x, G, F);
-        L.fl_ne = F.n_e;
-        const bool bound_flag = F.n_e == 0.0;
-        double theta = 0.0, nu = 0.0;
-        if (!bound_flag) {
-            theta = bk_angle(L.k, F, P.b_unit);
-            nu = fluid_nu(L.k, F);
+}
+
+/* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
+ * completed a step, the rest of the while-loop body of track_super_photon
+ * (harm_model.cpp:919-1063).  A lane that has to halve its step (push_photon's recursion,
+ * :1279-1285) spends extra trips while the other lanes of the wave keep stepping, instead of the
+ * whole wave waiting for the deepest halving tree.  Returns false when the photon's life ended. */
+__device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *wstack, int *wtop,
+                               unsigned long long &steps, unsigned long long &children, const Slot &ph2,
+                               const Slot &bk, double bias_d) {
+    if (L.phase == 0) {
+        if (stop_criterion(P, L)) {
+            end_of_life(P, C, cold, L);
+            return false;
         }
-        double d_tau_scatt, d_tau_abs, bias;
-        if (bound_flag || nu < 0.0) {
-            d_tau_scatt = 0.5 * L.alpha_scatti * P.d_tau_k * dl;
-            d_tau_abs = 0.5 * L.alpha_absi * P.d_tau_k * dl;
-            L.alpha_scatti = 0.0;
-            L.alpha_absi = 0.0;
-            bias = 0.0;
-            L.bi = 0.0;
-        } else {
-            const double a_sf = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
-            d_tau_scatt = 0.5 * (L.alpha_scatti + a_sf) * P.d_tau_k * dl;
-            L.alpha_scatti = a_sf;
-            const double a_af = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
-            d_tau_abs = 0.5 * (L.alpha_absi + a_af) * P.d_tau_k * dl;
-            L.alpha_absi = a_af;
-            const double bf = bias_func(P, C, F.theta_e, L.w);
-            bias = 0.5 * (L.bi + bf);
-            L.bi = bf;
+        /* photon_2 (:920-925) -- also the depth-0 backup of the push */
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ph2[i] = L.x[i];
+            ph2[4 + i] = L.k[i];
+            ph2[8 + i] = L.dk[i];
         }
-        const double x1 = -log(uniform(L.rng));
-        const double wc = L.w / bias;
-        if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) {
-            const double frac = x1 / (bias * d_tau_scatt);
-            d_tau_abs *= frac;
-            if (d_tau_abs > 100) {
-                trace_end(C, cold, L, 2);
-                return false; /* absorbed before scattering */
-            }
-            d_tau_scatt *= frac;
-            const double d_tau = d_tau_abs + d_tau_scatt;
-            if (d_tau_abs < 1.0e-3)
-                L.w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
-            else
-                L.w *= exp(-d_tau);
+        ph2[12] = L.e_0_s;
+        L.dl = step_size(P, L.x, L.k);
+        L.hlen = L.dl;
+        L.depth = 0;
+        L.pend = 0;
+        L.phase = 1;
+    }
+    TSTAMP(8);
+    /* one attempt of push_photon at the current node of the halving tree (:1217-1289) */
+    Trig T;
+    Gcov G;
+    bool have_tg = false;
+    if (!(L.x[1] < P.xs1)) {
+        if (L.depth > 0) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                L.x[i] = ph2[i];
-                L.k[i] = ph2[4 + i];
-                L.dk[i] = ph2[8 + i];
+                bk[i] = L.x[i];
+                bk[4 + i] = L.k[i];
+                bk[8 + i] = L.dk[i];
             }
-            L.e_0_s = ph2[12];
-            push_photon(P, L.x, L.k, L.dk, L.e_0_s, dl * frac, bk);
-            trig_at(P, L.x, T);
-            gcov_from_trig(P, T, G);
+        }
+        double e_1;
+        const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -L.depth), e_1, T, G);
+        TSTAMP(9);
+        if (fail && L.depth < MAX_SUBDIV) {
+            const Slot &src = L.depth == 0 ? ph2 : bk;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                L.x[i] = src[i];
+                L.k[i] = src[4 + i];
+                L.dk[i] = src[8 + i];
+            }
+            ++L.depth;
+            L.pend |= 1u << L.depth;
+            return true;
+        }
+        L.e_0_s = e_1;
+        have_tg = true;
+    }
+    if (L.pend) {
+        L.depth = 31 - __builtin_clz(L.pend);
+        L.pend &= ~(1u << L.depth);
+        return true;
+    }
+    /* the push is complete */
+    if (!have_tg) {
+        trig_at(P, L.x, T);
+        gcov_from_trig(P, T, G);
+    }
+    TSTAMP(10);
+    Fluid F;
+    if (L.phase == 2) {
+        /* back at the scattering point (:1007-1055) */
+        fluid_params(P, L.x, G, F);
+        L.fl_ne = F.n_e;
+        if (F.n_e > 0.0) {
+            /* scatter_super_photon's parent-side check (:1076-1081) */
+            if (L.k[0] > 1.0e5 || L.k[0] < 0.0 || isnan(L.k[0]) || isnan(L.k[1]) || isnan(L.k[3])) {
+                L.k[0] = fabs(L.k[0]);
+                L.w = 0.0;
+                trace_end(C, cold, L, 2);
+                return false;
+            }
+            push_request(C, L, cold, F, L.p_wc, wstack, wtop);
+            ++children;
+        }
+        const double theta = bk_angle(L.k, F, P.b_unit);
+        const double nu = fluid_nu(L.k, F);
+        if (nu < 0.0) {
+            L.alpha_scatti = 0.0;
+            L.alpha_absi = 0.0;
+        } else {
+            L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
+            L.alpha_absi = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
+        }
+        L.bi = bias_func(bias_d, F.theta_e, L.w);
+        L.tau_abs += L.p_dtau_abs;
+        L.tau_scatt += L.p_dtau_scatt;
+    } else {
+        ++steps;
+        if (stop_criterion(P, L)) {
+            end_of_life(P, C, cold, L);
+            return false;
+        }
+        if (L.alpha_absi > 0.0 || L.alpha_scatti > 0.0 || L.fl_ne > 0.0) {
             fluid_params(P, L.x, G, F);
             L.fl_ne = F.n_e;
-            if (F.n_e > 0.0) {
-                /* scatter_super_photon's parent-side check (:1076-1081) */
-                if (L.k[0] > 1.0e5 || L.k[0] < 0.0 || isnan(L.k[0]) || isnan(L.k[1]) || isnan(L.k[3])) {
-                    L.k[0] = fabs(L.k[0]);
-                    L.w = 0.0;
-                    trace_end(C, cold, L, 2);
-                    return false;
-                }
-                /* defer the child's sampling: push a scatter request (its stream id is fixed now) */
-                SReq R;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    R.x[i] = L.x[i];
-                    R.k[i] = L.k[i];
-                    R.u_con[i] = F.u_con[i];
-                    R.b_con[i] = F.b_con[i];
-                }
-                R.b = F.b;
-                R.theta_e = F.theta_e;
-                R.w = wc;
-                R.n_e_0 = cold->n_e_0;
-                R.theta_e_0 = cold->theta_e_0;
-                R.e_0 = cold->e_0;
-                R.id = child_id(L.rng.id, L.rng.ctr);
-                R.parent = L.rng.id;
-                R.n_scatt = L.n_scatt + 1;
-                R.pad0 = 0;
-                R.pad1 = 0.0;
-                atomicAdd(&C.ctr->n_children, 1ull);
-                if (sdepth < STACK_DEPTH) {
-                    store_sreq(my_stack + sdepth, R);
-                    ++sdepth;
-                } else {
-                    const unsigned long long o = atomicAdd(C.ovf_count, 1ull);
-                    if (o < C.ovf_cap)
-                        store_sreq(C.ovf + o, R);
-                    else
-                        atomicAdd(&C.ctr->n_dropped, 1ull);
-                    atomicAdd(&C.ctr->n_overflow, 1ull);
-                }
+            TSTAMP(11);
+            const bool bound_flag = F.n_e == 0.0;
+            double theta = 0.0, nu = 0.0;
+            if (!bound_flag) {
+                theta = bk_angle(L.k, F, P.b_unit);
+                nu = fluid_nu(L.k, F);
             }
-            theta = bk_angle(L.k, F, P.b_unit);
-            nu = fluid_nu(L.k, F);
-            if (nu < 0.0) {
+            const double dl = L.dl;
+            double d_tau_scatt, d_tau_abs, bias;
+            if (bound_flag || nu < 0.0) {
+                d_tau_scatt = 0.5 * L.alpha_scatti * P.d_tau_k * dl;
+                d_tau_abs = 0.5 * L.alpha_absi * P.d_tau_k * dl;
                 L.alpha_scatti = 0.0;
                 L.alpha_absi = 0.0;
+                bias = 0.0;
+                L.bi = 0.0;
             } else {
-                L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
-                L.alpha_absi = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
+                const double a_sf = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
+                d_tau_scatt = 0.5 * (L.alpha_scatti + a_sf) * P.d_tau_k * dl;
+                L.alpha_scatti = a_sf;
+                const double a_af = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
+                d_tau_abs = 0.5 * (L.alpha_absi + a_af) * P.d_tau_k * dl;
+                L.alpha_absi = a_af;
+                const double bf = bias_func(bias_d, F.theta_e, L.w);
+                bias = 0.5 * (L.bi + bf);
+                L.bi = bf;
             }
-            L.bi = bias_func(P, C, F.theta_e, L.w);
-        } else {
+            TSTAMP(12);
+            const double x1 = -log(uniform(L.rng));
+            const double wc = L.w / bias;
+            if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) {
+                const double frac = x1 / (bias * d_tau_scatt);
+                d_tau_abs *= frac;
+                if (d_tau_abs > 100) {
+                    trace_end(C, cold, L, 2);
+                    return false; /* absorbed before scattering */
+                }
+                d_tau_scatt *= frac;
+                const double d_tau = d_tau_abs + d_tau_scatt;
+                if (d_tau_abs < 1.0e-3)
+                    L.w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+                else
+                    L.w *= exp(-d_tau);
+                /* re-push photon_2 by dl*frac to the scattering point (:1005), on later trips */
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    L.x[i] = ph2[i];
+                    L.k[i] = ph2[4 + i];
+                    L.dk[i] = ph2[8 + i];
+                }
+                L.e_0_s = ph2[12];
+                L.hlen = dl * frac;
+                L.depth = 0;
+                L.pend = 0;
+                L.phase = 2;
+                L.p_dtau_abs = d_tau_abs;
+                L.p_dtau_scatt = d_tau_scatt;
+                L.p_wc = wc;
+                return true;
+            }
             if (d_tau_abs > 100) {
                 trace_end(C, cold, L, 2);
                 return false; /* absorbed */
@@ -508,10 +622,12 @@ __device__ bool transport_step(const Params &P, const Ctl &C, Lane &L, Cold *col
                 L.w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
             else
                 L.w *= exp(-d_tau);
+            L.tau_abs += d_tau_abs;
+            L.tau_scatt += d_tau_scatt;
         }
-        L.tau_abs += d_tau_abs;
-        L.tau_scatt += d_tau_scatt;
     }
+    TSTAMP(13);
+    L.phase = 0;
     ++L.n_step;
     if (L.n_step > MAX_N_STEP) {
         trace_end(C, cold, L, 3);
@@ -524,81 +640,124 @@ __device__ bool transport_step(const Params &P, const Ctl &C, Lane &L, Cold *col
 constexpr int LDS_DOUBLES_PER_LANE = 25;
 
 __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P, Ctl C) {
+#ifdef GRM_TIMING
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) < 16) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
+#endif
     __shared__ double lds[LDS_DOUBLES_PER_LANE * BLOCK];
     const Slot ph2{lds + threadIdx.x, BLOCK};
     const Slot bk{lds + 13 * BLOCK + threadIdx.x, BLOCK};
     const unsigned lane_id = threadIdx.x & 63;
     const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    SReq *my_stack = C.stack + gtid * STACK_DEPTH;
+    const int wave = threadIdx.x >> 6;
+    SReq *wstack = C.stack + (gtid >> 6) * WSTACK_CAP;
+    __shared__ int s_wtop[BLOCK / 64];
+    int *wtop = s_wtop + wave;
+    if (lane_id == 0) *wtop = 0;
     Cold *cold = C.cold + gtid;
     Lane L;
     L.rng.k0 = C.key0;
     L.rng.k1 = C.key1;
     bool active = false;
     bool pool_done = false; /* wave-uniform */
-    int sdepth = 0;
-    unsigned long long steps = 0, tracked = 0, primaries = 0;
+    double bias_d = bias_den(P, C); /* wave-uniform, refreshed every 16 trips when live */
+    unsigned trip = 1;
+    unsigned long long steps = 0, tracked = 0, primaries = 0, children = 0;
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
 
     while (true) {
-        /* refill, children first: pop a scatter request and sample the child */
-        if (!active && sdepth > 0) {
-            --sdepth;
-            SReq R;
-            load_sreq(my_stack + sdepth, R);
-            if (sample_child(P, C, R, L, cold)) {
-                active = init_photon(P, C, cold, L);
-            } else if (C.trace) {
-                write_trace(C, cold, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4, -1, -1);
-            }
-            ++tracked;
+        TCOUNT(4);
+        if ((trip++ & 15) == 0 && !C.bias_frozen) {
+            bias_d = bias_den(P, C);
+            TSTAMP(7);
         }
-        /* then the shared pool: one atomic per wave */
-        const bool want = !active && !pool_done;
-        const unsigned long long mask = __ballot(want);
-        if (mask) {
-            const int cnt = __popcll(mask);
-            const int leader = __ffsll((long long)mask) - 1;
-            unsigned long long base = 0;
-            if ((int)lane_id == leader) base = atomicAdd(C.pool_head, (unsigned long long)cnt);
-            base = __shfl(base, leader);
-            if (base + cnt >= C.n_pool) pool_done = true;
-            if (want) {
-                const unsigned long long idx = base + __popcll(mask & lt_mask);
-                if (idx < C.n_pool) {
-                    bool ok = true;
-                    if (C.pool_kind == 0) {
-                        load_primary(C, idx, L, cold);
-                        ++primaries;
-                    } else {
-                        SReq R;
-                        load_sreq(reinterpret_cast<const SReq *>(C.pool) + idx, R);
-                        ok = sample_child(P, C, R, L, cold);
-                        if (!ok && C.trace)
-                            write_trace(C, cold, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4, -1, -1);
-                    }
-                    if (ok) active = init_photon(P, C, cold, L);
-                    ++tracked;
+        /* Batched refill (converged point).  Idle lanes wait until at least refill_min of them can
+         * be refilled together -- children from the wave's stack first (depth-first order, like the
+         * reference's recursion, harm_model.cpp:1023), then primaries from the shared pool -- so the
+         * divergent child sampling and the photon set-up run once for a group of lanes instead of
+         * once per lane.  With no lane active, or once the pool is drained and every waiting child
+         * fits, the wave refills whatever it can. */
+        const unsigned long long idle = __ballot(!active);
+        if (idle) {
+            int top = *wtop;
+            if (top > WSTACK_CAP) top = WSTACK_CAP;
+            const int n_idle = __popcll(idle);
+            const int k_child = n_idle < top ? n_idle : top;
+            const int k_pool = pool_done ? 0 : n_idle - k_child;
+            const bool none_active = idle == __ballot(1);
+            if (k_child + k_pool >= C.refill_min || none_active || (pool_done && top > 0 && top <= n_idle)) {
+                const int r = __popcll(idle & lt_mask);
+                unsigned long long base = 0;
+                if (k_pool > 0) {
+                    if (lane_id == 0) base = atomicAdd(C.pool_head, (unsigned long long)k_pool);
+                    base = __shfl(base, 0);
+                    if (base + k_pool >= C.n_pool) pool_done = true;
                 }
+                if (lane_id == 0) *wtop = top - k_child;
+#ifdef GRM_TIMING
+                if (k_child) TCOUNT(5);
+                if (k_pool) TCOUNT(6);
+#endif
+                bool has = false, ok = true;
+                if (!active && r < k_child) {
+                    SReq R;
+                    load_sreq(wstack + (top - 1 - r), R);
+                    ok = sample_child(P, C, R, L, cold);
+                    if (!ok && C.trace)
+                        write_trace(C, cold, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4, -1, -1);
+                    has = true;
+                }
+                TSTAMP(0);
+                if (!active && r >= k_child && k_pool > 0) {
+                    const unsigned long long idx = base + (unsigned long long)(r - k_child);
+                    if (idx < C.n_pool) {
+                        if (C.pool_kind == 0) {
+                            load_primary(C, idx, L, cold);
+                            ++primaries;
+                        } else {
+                            SReq R;
+                            load_sreq(reinterpret_cast<const SReq *>(C.pool) + idx, R);
+                            ok = sample_child(P, C, R, L, cold);
+                            if (!ok && C.trace)
+                                write_trace(C, cold, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4,
+                                            -1, -1);
+                        }
+                        has = true;
+                    }
+                }
+                if (has) {
+                    ++tracked;
+                    if (ok) active = init_photon(P, C, cold, L, bias_d);
+                }
+                TSTAMP(1);
             }
         }
         if (!__any(active)) {
-            if (pool_done && !__any(sdepth > 0)) break;
+            if (pool_done && *wtop == 0) break;
             continue;
         }
-        if (active) active = transport_step(P, C, L, cold, my_stack, sdepth, steps, ph2, bk);
+        if (active) active = transport_trip(P, C, L, cold, wstack, wtop, steps, children, ph2, bk, bias_d);
+        TSTAMP(2);
     }
+#ifdef GRM_TIMING
+    if (lane_id == 0) {
+        g_tlds[threadIdx.x >> 6][3] = __builtin_amdgcn_s_memtime() - t_start;
+        for (int r = 0; r < 15; ++r) atomicAdd(C.timing + r, g_tlds[threadIdx.x >> 6][r]);
+    }
+#endif
     /* wave-reduce the lane counters, one atomic per wave */
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         steps += __shfl_xor(steps, off);
         tracked += __shfl_xor(tracked, off);
         primaries += __shfl_xor(primaries, off);
+        children += __shfl_xor(children, off);
     }
     if (lane_id == 0) {
         atomicAdd(&C.ctr->n_steps, steps);
         atomicAdd(&C.ctr->n_tracked, tracked);
         atomicAdd(&C.ctr->n_primaries, primaries);
+        atomicAdd(&C.ctr->n_children, children);
     }
 }
 
@@ -633,12 +792,14 @@ struct grm_engine {
     double max_tau_init = 0.0;
     bool frozen_set = false;
     int64_t warmup = -1;     /* photons; -1 = lanes */
+    int refill_min = 16;
     uint64_t history = 0;    /* primaries tracked since reset */
     double fz_scatt = 0.0, fz_rec = 0.0, fz_maxtau = 0.0;
     grm_stats stats{};
     grm_init_photon *d_upload = nullptr;
     size_t upload_cap = 0;
     ncclComm_t comm = nullptr;
+    unsigned long long *d_timing = nullptr;
     std::string err;
 };
 
@@ -708,6 +869,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     C.trace = e->trace_cap ? e->d_trace : nullptr;
     C.trace_cap = e->trace_cap;
     C.trace_count = e->d_small + 3;
+    C.timing = e->d_timing;
+    C.refill_min = e->refill_min;
     C.bias_frozen = e->bias_mode;
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
@@ -871,6 +1034,9 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     P.zones = e->d_zones;
     P.hotcross = e->d_hot;
     P.k2 = e->d_k2;
+    if (!hip_ok(e, hipMalloc(&e->d_timing, 16 * sizeof(unsigned long long)), "timing") ||
+        !hip_ok(e, hipMemset(e->d_timing, 0, 16 * sizeof(unsigned long long)), "timing"))
+        return fail();
     if (reset_counters(e)) return fail();
     *out = e;
     return 0;
@@ -893,6 +1059,7 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_batch);
     hipFree(e->d_trace);
     hipFree(e->d_upload);
+    hipFree(e->d_timing);
     if (e->comm) ncclCommDestroy(e->comm);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
@@ -923,6 +1090,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_FROZEN_REC: e->fz_rec = (double)v; e->frozen_set = true; return 0;
     case GRM_OPT_FROZEN_MAXTAU: std::memcpy(&e->fz_maxtau, &v, sizeof(double)); e->frozen_set = true; return 0;
     case GRM_OPT_WARMUP: e->warmup = v; return 0;
+    case GRM_OPT_REFILL_MIN: e->refill_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     default: e->err = "unknown option"; return -1;
     }
 }
@@ -1013,6 +1181,18 @@ int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm
     HIPCHK(e, hipMemcpy(e->d_upload, batch, n * sizeof(grm_init_photon), hipMemcpyHostToDevice));
     *dev_out = e->d_upload;
     return 0;
+}
+
+int grm_engine_debug_timing(grm_engine *e, uint64_t out[16], int reset) {
+    if (!e || !out) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemcpy(out, e->d_timing, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(e, hipMemset(e->d_timing, 0, 16 * sizeof(unsigned long long)));
+#ifdef GRM_TIMING
+    return 1;
+#else
+    return 0;
+#endif
 }
 
 int grm_rccl_unique_id(uint8_t id_out[128]) {

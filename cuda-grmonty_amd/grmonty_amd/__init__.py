@@ -38,6 +38,7 @@ TRACE = np.dtype([("id", "<u8"), ("parent_id", "<u8"), ("w", "<f8"), ("e", "<f8"
                   ("n_step", "<i4"), ("end_reason", "<i4"), ("ix2", "<i4"), ("i_e", "<i4"), ("pad_", "<i4")])
 
 OPT_SEED, OPT_BIAS_MODE, OPT_TRACE_CAP, OPT_GRID_BLOCKS, OPT_ID_BASE = 0, 1, 2, 3, 4
+OPT_FROZEN_SCATT, OPT_FROZEN_REC, OPT_FROZEN_MAXTAU, OPT_WARMUP, OPT_REFILL_MIN = 5, 6, 7, 8, 9
 N_TH_BINS, N_E_BINS = 6, 200
 
 
@@ -97,6 +98,7 @@ SIGNATURES = {
     "grm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "grm_engine_comm_init": (C.c_int, [VP, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     "grm_engine_allreduce": (C.c_int, [VP]),
+    "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
     "grm_sizeof": (C.c_size_t, [C.c_int]),
     "grm_version": (C.c_char_p, []),
 }
@@ -288,6 +290,11 @@ class Engine:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._check(self.L.grm_engine_comm_init(self.h, buf, nranks, rank))
+
+    def debug_timing(self, reset: bool = True):
+        out = (C.c_uint64 * 16)()
+        instrumented = self.L.grm_engine_debug_timing(self.h, out, 1 if reset else 0)
+        return instrumented, list(out)
 
     def allreduce(self):
         self._check(self.L.grm_engine_allreduce(self.h))

@@ -128,7 +128,10 @@ enum {
     /* live-bias warm-up: until this many photons have been tracked since the last reset, a
      * batch is cut into launches that double the history each time, so the adaptive bias
      * counters evolve as in the serial reference (-1 = one persistent grid's worth of lanes, 0 = off) */
-    GRM_OPT_WARMUP = 8
+    GRM_OPT_WARMUP = 8,
+    /* idle lanes a wavefront gathers before it refills them together (1..64, default 16):
+     * larger = less divergent child sampling / photon set-up, more idle lane-trips */
+    GRM_OPT_REFILL_MIN = 9
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
@@ -161,6 +164,10 @@ int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap);
 /* copy a host batch into an engine-owned device buffer once (inputs resident in HBM); *dev_out is
  * valid for grm_engine_track_device until the next upload or destroy. */
 int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm_init_photon **dev_out);
+
+/* diagnostic: per-region wave cycles of a -DGRM_TIMING build, 16 slots (returns 1 if the build
+ * is instrumented, 0 if not; out[] then stays zero) */
+int grm_engine_debug_timing(grm_engine *e, uint64_t out[16], int reset);
 
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
 /* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */

@@ -23,7 +23,10 @@ print(f"emit {len(ph)} photons {time.time() - t:.2f}s", flush=True)
 e = G.Engine(m, 0)
 if grid:
     e.set_option(G.OPT_GRID_BLOCKS, grid)
-for rep in range(3):
+if os.environ.get("REFILL_MIN"):
+    e.set_option(G.OPT_REFILL_MIN, int(os.environ["REFILL_MIN"]))
+    print(f"refill_min {os.environ['REFILL_MIN']}", flush=True)
+for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
     e.reset()
     t = time.time()
     e.track(ph)
@@ -34,3 +37,11 @@ for rep in range(3):
           f"({st['last_steps'] / st['last_kernel_ms'] / 1e3:.3g} Msteps/s) tracked {st['n_tracked']} "
           f"children {st['n_children']} overflow {st['n_overflow']} launches {st['n_launches']} "
           f"rate {len(ph) / (st['last_kernel_ms'] * 1e-3):.4g} ph/s rec {nr} scatt {ns}", flush=True)
+    inst, tm = e.debug_timing(reset=True)
+    if inst:
+        tot = max(tm[3], 1)
+        names = {0: "child", 1: "init", 2: "trip-tail", 7: "bias", 8: "phase0", 9: "attempt", 10: "restore",
+                 11: "fluid", 12: "radiation", 13: "interact"}
+        print("  timing: " + " ".join(f"{v}={tm[k] / tot:.3f}" for k, v in names.items()) +
+              f" | trips/wave {tm[4]} child-refills {tm[5] / max(tm[4], 1):.4f} pool-refills "
+              f"{tm[6] / max(tm[4], 1):.4f} cycles/trip {tot / max(tm[4], 1):.0f}", flush=True)
