@@ -20,6 +20,7 @@ namespace grm {
 
 /* ---- constants: reference consts.hpp:14-157 (same literals) ---- */
 constexpr double kPi = 3.141592653589793238462643383279502884;
+constexpr double kLog10E = 0.43429448190325182765112891891660508; /* 1 / ln 10 */
 constexpr double kSqrt2 = 1.414213562373095048801688724209698079;
 constexpr double EPS = 1.0e-40;
 constexpr double THETA_E_MIN = 0.3, TP_OVER_TE = 3.0;
@@ -284,8 +285,15 @@ __device__ __forceinline__ double step_size(const Params &P, const double x[4], 
 
 /* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
  * predicate of :1279 and the new energy e_1; leaves Gcov at the new x in G. */
+struct NoPrefetch {
+    __device__ __forceinline__ void operator()(const double *) const {}
+};
+
+/* `pre(x)` runs as soon as the new position is known (before the connection and the corrector),
+ * so the caller can issue the fluid gather at x early and let this attempt's VALU work hide it. */
+template <class Pre = NoPrefetch>
 __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
-                                             double dl, double &e_1, Trig &T, Gcov &G) {
+                                             double dl, double &e_1, Trig &T, Gcov &G, Pre &&pre = Pre()) {
     const double dl_2 = 0.5 * dl;
     double kp[4];
 #pragma unroll
@@ -295,6 +303,7 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
         kp[i] = k[i] + d;
         x[i] += k[i] * dl;
     }
+    pre(x);
     trig_at(P, x, T);
     Conn C;
     connection(P, T, C);
@@ -375,17 +384,12 @@ struct Fluid {
     double u_con[4], u_cov[4], b_con[4], b_cov[4];
 };
 
-__device__ __forceinline__ void fluid_params(const Params &P, const double x[4], const Gcov &G, Fluid &F) {
-    if (x[1] < P.xs1 || x[1] > P.xe1 || x[2] < P.xs2 || x[2] > P.xe2) {
-        /* out of grid: n_e = 0; the reference leaves the rest unset, we zero it (so does the oracle) */
-        F.n_e = F.theta_e = F.b = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) F.u_con[q] = F.u_cov[q] = F.b_con[q] = F.b_cov[q] = 0.0;
-        return;
-    }
-    int i = (int)((x[1] - P.xs1) / P.dx1 - 0.5 + 1000) - 1000;
-    int j = (int)((x[2] - P.xs2) / P.dx2 - 0.5 + 1000) - 1000;
-    double di, dj;
+/* cell-centred zone index and bilinear weights of x (x_to_ij, harm_model.cpp:1406-1434, with the
+ * edge clamp of interp_scalar); false = out of the grid */
+__device__ __forceinline__ bool zone_index(const Params &P, const double x[4], int &i, int &j, double &di, double &dj) {
+    if (x[1] < P.xs1 || x[1] > P.xe1 || x[2] < P.xs2 || x[2] > P.xe2) return false;
+    i = (int)((x[1] - P.xs1) / P.dx1 - 0.5 + 1000) - 1000;
+    j = (int)((x[2] - P.xs2) / P.dx2 - 0.5 + 1000) - 1000;
     if (i < 0) {
         i = 0;
         di = 0.0;
@@ -404,14 +408,45 @@ __device__ __forceinline__ void fluid_params(const Params &P, const double x[4],
     } else {
         dj = (x[2] - ((j + 0.5) * P.dx2 + P.xs2)) / P.dx2;
     }
+    return true;
+}
+
+/* the 4 zones around x: (i,j),(i,j+1) and (i+1,j),(i+1,j+1) are two contiguous 128-B runs of the
+ * zone-major [n1][n2][8] field array, 8 x 16-B loads each */
+struct ZoneFetch {
+    double2 v[16];
+};
+
+__device__ __forceinline__ void zone_fetch(const Params &P, const double x[4], ZoneFetch &Z) {
+    int i, j;
+    double di, dj;
+    if (!zone_index(P, x, i, j, di, dj)) return;
+    const double2 *z0 = reinterpret_cast<const double2 *>(P.zones + ((size_t)i * P.n2 + j) * 8);
+    const double2 *z1 = reinterpret_cast<const double2 *>(P.zones + ((size_t)(i + 1) * P.n2 + j) * 8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        Z.v[q] = z0[q];
+        Z.v[8 + q] = z1[q];
+    }
+}
+
+/* get_fluid_params (harm_model.cpp:595-671) from fetched zones */
+__device__ __forceinline__ void fluid_from(const Params &P, const double x[4], const Gcov &G, const ZoneFetch &Z,
+                                           Fluid &F) {
+    int i, j;
+    double di, dj;
+    if (!zone_index(P, x, i, j, di, dj)) {
+        /* out of grid: n_e = 0; the reference leaves the rest unset, we zero it (so does the oracle) */
+        F.n_e = F.theta_e = F.b = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F.u_con[q] = F.u_cov[q] = F.b_con[q] = F.b_cov[q] = 0.0;
+        return;
+    }
     const double c0 = (1.0 - di) * (1.0 - dj), c1 = (1.0 - di) * dj, c2 = di * (1.0 - dj), c3 = di * dj;
-    /* 4 zones x 64 B, each as 4 x 16-B loads */
-    const double2 *z00 = reinterpret_cast<const double2 *>(P.zones + ((size_t)i * P.n2 + j) * 8);
-    const double2 *z10 = reinterpret_cast<const double2 *>(P.zones + ((size_t)(i + 1) * P.n2 + j) * 8);
     double v[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const double2 a = z00[q], b = z00[q + 4], c = z10[q], d = z10[q + 4];
+        const double2 a = Z.v[q], b = Z.v[q + 4], c = Z.v[8 + q], d = Z.v[12 + q];
         v[2 * q] = a.x * c0 + b.x * c1 + c.x * c2 + d.x * c3;
         v[2 * q + 1] = a.y * c0 + b.y * c1 + c.y * c2 + d.y * c3;
     }
@@ -438,6 +473,12 @@ __device__ __forceinline__ void fluid_params(const Params &P, const double x[4],
           P.b_unit;
 }
 
+__device__ __forceinline__ void fluid_params(const Params &P, const double x[4], const Gcov &G, Fluid &F) {
+    ZoneFetch Z;
+    zone_fetch(P, x, Z);
+    fluid_from(P, x, G, Z, F);
+}
+
 /* ------------------------------------------------------------------------- */
 /* radiation (radiation.cpp:59-146), hotcross lookup (hotcross.cpp:81-106),   */
 /* synchrotron (jnu_mixed.cpp:75-111, 150-158)                                */
@@ -448,6 +489,16 @@ __device__ __forceinline__ double bk_angle(const double k[4], const Fluid &F, do
     double mu = (k[0] * F.b_cov[0] + k[1] * F.b_cov[1] + k[2] * F.b_cov[2] + k[3] * F.b_cov[3]) / (k_ * F.b / b_unit);
     mu = fmin(fmax(mu, -1.0), 1.0);
     return acos(mu);
+}
+
+/* sin(bk_angle): the synchrotron emissivity only needs sin(theta) = sqrt(1 - mu^2), theta in
+ * [0, pi]; saves the acos + sin pair (theta = pi/2 when b = 0, as bk_angle) */
+__device__ __forceinline__ double bk_sin(const double k[4], const Fluid &F, double b_unit) {
+    if (F.b == 0.0) return 1.0;
+    const double k_ = fabs(k[0] * F.u_cov[0] + k[1] * F.u_cov[1] + k[2] * F.u_cov[2] + k[3] * F.u_cov[3]);
+    double mu = (k[0] * F.b_cov[0] + k[1] * F.b_cov[1] + k[2] * F.b_cov[2] + k[3] * F.b_cov[3]) / (k_ * F.b / b_unit);
+    mu = fmin(fmax(mu, -1.0), 1.0);
+    return sqrt((1.0 - mu) * (1.0 + mu));
 }
 
 __device__ __forceinline__ double fluid_nu(const double k[4], const Fluid &F) {
@@ -494,12 +545,13 @@ __device__ __noinline__ double hotcross_num(double w, double theta_e) {
     return cross * SIGMA_THOMSON;
 }
 
-__device__ __forceinline__ double hotcross_lkup(const Params &P, double w, double theta_e) {
+/* ln_te = ln(theta_e), shared with k2_eval */
+__device__ __forceinline__ double hotcross_lkup(const Params &P, double w, double theta_e, double ln_te) {
     if (w * theta_e < 1.0e-6) return SIGMA_THOMSON;
     if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
     if (w <= HC_MIN_W || w >= HC_MAX_W || theta_e <= HC_MIN_T || theta_e >= HC_MAX_T) return hotcross_num(w, theta_e);
     const double fi = (log10(w) - P.hc_l_min_w) / P.hc_d_l_w;
-    const double fj = (log10(theta_e) - P.hc_l_min_t) / P.hc_d_l_t;
+    const double fj = (ln_te * kLog10E - P.hc_l_min_t) / P.hc_d_l_t;
     const int i = (int)fi, j = (int)fj;
     const double d_i = fi - i, d_j = fj - j;
     const double *t = P.hotcross + (size_t)i * (HC_N_T + 1) + j;
@@ -509,21 +561,28 @@ __device__ __forceinline__ double hotcross_lkup(const Params &P, double w, doubl
     return exp10(lc);
 }
 
-__device__ __forceinline__ double k2_eval(const Params &P, double theta_e) {
+__device__ __forceinline__ double hotcross_lkup(const Params &P, double w, double theta_e) {
+    return hotcross_lkup(P, w, theta_e, log(theta_e));
+}
+
+__device__ __forceinline__ double k2_eval(const Params &P, double theta_e, double ln_te) {
     if (theta_e < THETA_E_MIN) return 0.0;
     if (theta_e > JNU_MAX_T) return 2.0 * theta_e * theta_e;
-    double d_i = (log(theta_e) - P.jnu_l_min_t) / P.jnu_d_l_t;
+    double d_i = (ln_te - P.jnu_l_min_t) / P.jnu_d_l_t;
     const int i = min((int)d_i, GRM_N_E_SAMP - 1); /* theta_e == 100 exactly: stay in the table */
     d_i -= i;
     return exp((1.0 - d_i) * P.k2[i] + d_i * P.k2[i + 1]);
 }
 
-__device__ __forceinline__ double synch(const Params &P, double nu, double n_e, double theta_e, double b,
-                                        double theta) {
+__device__ __forceinline__ double k2_eval(const Params &P, double theta_e) { return k2_eval(P, theta_e, log(theta_e)); }
+
+/* jnu_mixed::synch with sin(theta) and ln(theta_e) supplied */
+__device__ __forceinline__ double synch_s(const Params &P, double nu, double n_e, double theta_e, double b,
+                                          double sin_theta, double ln_te) {
     if (theta_e < THETA_E_MIN) return 0.0;
-    const double k2 = k2_eval(P, theta_e);
+    const double k2 = k2_eval(P, theta_e, ln_te);
     const double nu_c = EE * b / (2.0 * kPi * ME * CL);
-    const double nu_s = (2.0 / 9.0) * nu_c * theta_e * theta_e * sin(theta);
+    const double nu_s = (2.0 / 9.0) * nu_c * theta_e * theta_e * sin_theta;
     if (nu > 1.0e12 * nu_s) return 0.0;
     const double x = nu / nu_s;
     const double xp = cbrt(x);
@@ -532,15 +591,26 @@ __device__ __forceinline__ double synch(const Params &P, double nu, double n_e, 
     return (kSqrt2 * kPi * EE * EE * n_e * nu_s / (3.0 * CL * k2)) * f * exp(-xp);
 }
 
-__device__ __forceinline__ double alpha_inv_scatt(const Params &P, double nu, double theta_e, double n_e) {
+__device__ __forceinline__ double synch(const Params &P, double nu, double n_e, double theta_e, double b,
+                                        double theta) {
+    return synch_s(P, nu, n_e, theta_e, b, sin(theta), log(theta_e));
+}
+
+__device__ __forceinline__ double alpha_inv_scatt(const Params &P, double nu, double theta_e, double n_e,
+                                                  double ln_te) {
     const double e_g = HPL * nu / (ME * CL * CL);
-    const double kappa = hotcross_lkup(P, e_g, theta_e) / MP;
+    const double kappa = hotcross_lkup(P, e_g, theta_e, ln_te) / MP;
     return nu * kappa * n_e * MP;
 }
 
-__device__ __forceinline__ double alpha_inv_abs(const Params &P, double nu, double theta_e, double n_e, double b,
-                                                double theta) {
-    const double j = synch(P, nu, n_e, theta_e, b, theta) / (nu * nu);
+__device__ __forceinline__ double alpha_inv_scatt(const Params &P, double nu, double theta_e, double n_e) {
+    return alpha_inv_scatt(P, nu, theta_e, n_e, log(theta_e));
+}
+
+/* alpha_inv_abs with sin(theta) and ln(theta_e) supplied */
+__device__ __forceinline__ double alpha_inv_abs_s(const Params &P, double nu, double theta_e, double n_e, double b,
+                                                  double sin_theta, double ln_te) {
+    const double j = synch_s(P, nu, n_e, theta_e, b, sin_theta, ln_te) / (nu * nu);
     const double x = HPL * nu / (ME * CL * CL * theta_e);
     double b_nu;
     if (x < 1.0e-3)
@@ -548,6 +618,11 @@ __device__ __forceinline__ double alpha_inv_abs(const Params &P, double nu, doub
     else
         b_nu = (2.0 * HPL / (CL * CL)) / (exp(x) - 1.0);
     return j / (b_nu + 1.0e-100);
+}
+
+__device__ __forceinline__ double alpha_inv_abs(const Params &P, double nu, double theta_e, double n_e, double b,
+                                                double theta) {
+    return alpha_inv_abs_s(P, nu, theta_e, n_e, b, sin(theta), log(theta_e));
 }
 
 /* ------------------------------------------------------------------------- */

@@ -42,8 +42,8 @@ namespace {
 #endif
 constexpr int BLOCK = 256;
 constexpr int MIN_WAVES_PER_SIMD = GRM_WAVES_PER_SIMD;
-constexpr int STACK_DEPTH = 8;                  /* scatter-request slots per lane ... */
-constexpr int WSTACK_CAP = 64 * STACK_DEPTH;    /* ... pooled into one stack per wave */
+constexpr int STACK_DEPTH = 16;                 /* scatter-request slots per lane ... */
+constexpr int WSTACK_CAP = 64 * STACK_DEPTH;    /* ... pooled into one stack per wave (208 KB of HBM) */
 
 /* 208-B scatter request: the state at a scattering event from which the child
  * photon is sampled later (scatter_super_photon, harm_model.cpp:1071-1145).
@@ -95,6 +95,8 @@ struct Ctl {
     double f_scatt, f_rec, f_maxtau;
     unsigned long long *timing; /* GRM_TIMING builds: per-region wave cycles */
     int refill_min;             /* idle lanes a wave gathers before it refills (batching) */
+    double *bk;                 /* push backup of the halving walk, [12][lanes] (rarely touched) */
+    int lanes;
 };
 
 /* hot photon state: lives in VGPRs for the photon's whole life */
@@ -220,14 +222,43 @@ __device__ __forceinline__ void trace_end(const Ctl &C, const Cold *cold, const 
                     reason, -1, -1);
 }
 
+/* Workgroup-private spectrum and per-wave counter deltas in LDS.  record_super_photon's twelve
+ * fp64 adds go to LDS (ds_add_f64) instead of global atomics: global float atomics execute at the
+ * memory side and stay counted in the wave's in-order vmcnt for ~1-3k cycles, so every later load
+ * of the wave (the next fluid gather) would wait for them.  The block adds its spectrum to the
+ * global one once, at exit; counter deltas are flushed by each wave at its bias-refresh points.
+ * Field f of a cell = field f of grm_spectrum_cell (e_0, never accumulated, is left out). */
+constexpr int SPEC_FIELDS = 12;
+constexpr int SPEC_LDS = N_TH_BINS * N_E_BINS * SPEC_FIELDS;
+__shared__ double s_spec[SPEC_LDS];
+__shared__ unsigned long long s_cnt[BLOCK / 64][4]; /* n_recorded, n_scatt, max tau bits, max flushed */
+
+__device__ __forceinline__ void flush_counters(const Ctl &C) {
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long *c = s_cnt[threadIdx.x >> 6];
+        if (c[0]) {
+            atomicAdd(&C.ctr->n_recorded, c[0]);
+            c[0] = 0;
+        }
+        if (c[1]) {
+            atomicAdd(&C.ctr->n_scatt, c[1]);
+            c[1] = 0;
+        }
+        if (c[2] > c[3]) {
+            atomicMax(&C.ctr->max_tau_bits, c[2]);
+            c[3] = c[2];
+        }
+    }
+}
+
 /* record_super_photon (harm_model.cpp:1291-1335) */
 __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, uint64_t id, double w, double x1,
                               double x2, double x3, double tau_abs, double tau_scatt, int n_scatt, int n_step) {
     int ix2 = -1, i_e = -1, reason = 1;
     const double e = cold->e;
     if (!(isnan(w) || isnan(e))) {
-        if (tau_scatt > __longlong_as_double((long long)C.ctr->max_tau_bits))
-            atomicMax(&C.ctr->max_tau_bits, (unsigned long long)__double_as_longlong(tau_scatt));
+        unsigned long long *cnt = s_cnt[threadIdx.x >> 6];
+        atomicMax(cnt + 2, (unsigned long long)__double_as_longlong(tau_scatt)); /* tau_scatt >= 0 */
         if (x2 < 0.5 * (P.xs2 + P.xe2))
             ix2 = (int)(x2 / P.th_dx2);
         else
@@ -236,22 +267,22 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
             i_e = (int)((log(e) - P.spec_l_e_0) / SPEC_D_L_E + 2.5) - 2;
             if (i_e >= 0 && i_e < N_E_BINS) {
                 reason = 0;
-                atomicAdd(&C.ctr->n_recorded, 1ull);
-                atomicAdd(&C.ctr->n_scatt, (unsigned long long)n_scatt);
-                grm_spectrum_cell *s = C.spec + ix2 * N_E_BINS + i_e;
+                atomicAdd(cnt + 0, 1ull);
+                atomicAdd(cnt + 1, (unsigned long long)n_scatt);
+                double *s = s_spec + (ix2 * N_E_BINS + i_e) * SPEC_FIELDS;
                 const double x1i = cold->x1i, x2i = cold->x2i;
-                unsafeAtomicAdd(&s->dn_dle, w);
-                unsafeAtomicAdd(&s->de_dle, w * e);
-                unsafeAtomicAdd(&s->tau_abs, w * tau_abs);
-                unsafeAtomicAdd(&s->tau_scatt, w * tau_scatt);
-                unsafeAtomicAdd(&s->x1i_av, w * x1i);
-                unsafeAtomicAdd(&s->x2i_sq, w * (x2i * x2i));
-                unsafeAtomicAdd(&s->x3f_sq, w * (x3 * x3));
-                unsafeAtomicAdd(&s->ne_0, w * cold->n_e_0);
-                unsafeAtomicAdd(&s->b_0, w * cold->b_0);
-                unsafeAtomicAdd(&s->theta_e_0, w * cold->theta_e_0);
-                unsafeAtomicAdd(&s->nscatt, (double)n_scatt);
-                unsafeAtomicAdd(&s->nph, 1.0);
+                atomicAdd(s + 0, w);                      /* dn_dle */
+                atomicAdd(s + 1, w * e);                  /* de_dle */
+                atomicAdd(s + 2, 1.0);                    /* nph */
+                atomicAdd(s + 3, (double)n_scatt);        /* nscatt */
+                atomicAdd(s + 4, w * x1i);                /* x1i_av */
+                atomicAdd(s + 5, w * (x2i * x2i));        /* x2i_sq */
+                atomicAdd(s + 6, w * (x3 * x3));          /* x3f_sq */
+                atomicAdd(s + 7, w * tau_abs);            /* tau_abs */
+                atomicAdd(s + 8, w * tau_scatt);          /* tau_scatt */
+                atomicAdd(s + 9, w * cold->n_e_0);        /* ne_0 */
+                atomicAdd(s + 10, w * cold->theta_e_0);   /* theta_e_0 */
+                atomicAdd(s + 11, w * cold->b_0);         /* b_0 */
             } else {
                 i_e = -1;
             }
@@ -284,10 +315,10 @@ __device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lan
     gcov_from_trig(P, T, G);
     Fluid F;
     fluid_params(P, L.x, G, F);
-    const double theta = bk_angle(L.k, F, P.b_unit);
     const double nu = fluid_nu(L.k, F);
-    L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
-    L.alpha_absi = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
+    const double ln_te = log(F.theta_e);
+    L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e, ln_te);
+    L.alpha_absi = alpha_inv_abs_s(P, nu, F.theta_e, F.n_e, F.b, bk_sin(L.k, F, P.b_unit), ln_te);
     L.bi = bias_func(bias_d, F.theta_e, L.w);
     L.fl_ne = F.n_e;
     Conn Cn;
@@ -477,6 +508,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     /* one attempt of push_photon at the current node of the halving tree (:1217-1289) */
     Trig T;
     Gcov G;
+    ZoneFetch Z;
     bool have_tg = false;
     if (!(L.x[1] < P.xs1)) {
         if (L.depth > 0) {
@@ -488,7 +520,8 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             }
         }
         double e_1;
-        const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -L.depth), e_1, T, G);
+        const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -L.depth), e_1, T, G,
+                                       [&](const double *xn) { zone_fetch(P, xn, Z); });
         TSTAMP(9);
         if (fail && L.depth < MAX_SUBDIV) {
             const Slot &src = L.depth == 0 ? ph2 : bk;
@@ -510,77 +543,78 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         L.pend &= ~(1u << L.depth);
         return true;
     }
-    /* the push is complete */
-    if (!have_tg) {
-        trig_at(P, L.x, T);
-        gcov_from_trig(P, T, G);
-    }
-    TSTAMP(10);
-    Fluid F;
-    if (L.phase == 2) {
-        /* back at the scattering point (:1007-1055) */
-        fluid_params(P, L.x, G, F);
-        L.fl_ne = F.n_e;
-        if (F.n_e > 0.0) {
-            /* scatter_super_photon's parent-side check (:1076-1081) */
-            if (L.k[0] > 1.0e5 || L.k[0] < 0.0 || isnan(L.k[0]) || isnan(L.k[1]) || isnan(L.k[3])) {
-                L.k[0] = fabs(L.k[0]);
-                L.w = 0.0;
-                trace_end(C, cold, L, 2);
-                return false;
-            }
-            push_request(C, L, cold, F, L.p_wc, wstack, wtop);
-            ++children;
-        }
-        const double theta = bk_angle(L.k, F, P.b_unit);
-        const double nu = fluid_nu(L.k, F);
-        if (nu < 0.0) {
-            L.alpha_scatti = 0.0;
-            L.alpha_absi = 0.0;
-        } else {
-            L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
-            L.alpha_absi = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
-        }
-        L.bi = bias_func(bias_d, F.theta_e, L.w);
-        L.tau_abs += L.p_dtau_abs;
-        L.tau_scatt += L.p_dtau_scatt;
-    } else {
+    /* the push is complete.  Phase 1 = end of a geodesic step: stop test, then the interaction
+     * block (:927-1056).  Phase 2 = back at the scattering point after the re-push (:1005-1055).
+     * Both evaluate the fluid and the absorption/scattering coefficients at the new point; they share
+     * ONE evaluation here so a wave with lanes in both phases runs that code once. */
+    const bool at_scatter = L.phase == 2;
+    if (!at_scatter) {
         ++steps;
         if (stop_criterion(P, L)) {
             end_of_life(P, C, cold, L);
             return false;
         }
-        if (L.alpha_absi > 0.0 || L.alpha_scatti > 0.0 || L.fl_ne > 0.0) {
-            fluid_params(P, L.x, G, F);
-            L.fl_ne = F.n_e;
-            TSTAMP(11);
-            const bool bound_flag = F.n_e == 0.0;
-            double theta = 0.0, nu = 0.0;
-            if (!bound_flag) {
-                theta = bk_angle(L.k, F, P.b_unit);
-                nu = fluid_nu(L.k, F);
+    }
+    TSTAMP(10);
+    if (at_scatter || L.alpha_absi > 0.0 || L.alpha_scatti > 0.0 || L.fl_ne > 0.0) {
+        if (!have_tg) {
+            trig_at(P, L.x, T);
+            gcov_from_trig(P, T, G);
+            zone_fetch(P, L.x, Z);
+        }
+        Fluid F;
+        fluid_from(P, L.x, G, Z, F);
+        L.fl_ne = F.n_e;
+        TSTAMP(11);
+        /* scatter_super_photon's parent-side check (:1076-1081) */
+        if (at_scatter && F.n_e > 0.0 &&
+            (L.k[0] > 1.0e5 || L.k[0] < 0.0 || isnan(L.k[0]) || isnan(L.k[1]) || isnan(L.k[3]))) {
+            L.k[0] = fabs(L.k[0]);
+            L.w = 0.0;
+            trace_end(C, cold, L, 2);
+            return false;
+        }
+        /* phase 1 skips the coefficients out of the fluid (bound_flag, :941-955); both skip them
+         * for nu < 0 */
+        const double nu = fluid_nu(L.k, F);
+        const bool zero = nu < 0.0 || (!at_scatter && F.n_e == 0.0);
+        double a_s = 0.0, a_a = 0.0;
+        if (!zero) {
+            const double sth = bk_sin(L.k, F, P.b_unit);
+            const double ln_te = log(F.theta_e);
+            a_s = alpha_inv_scatt(P, nu, F.theta_e, F.n_e, ln_te);
+            a_a = alpha_inv_abs_s(P, nu, F.theta_e, F.n_e, F.b, sth, ln_te);
+        }
+        const double bf = (zero && !at_scatter) ? 0.0 : bias_func(bias_d, F.theta_e, L.w);
+        TSTAMP(12);
+        if (at_scatter) {
+            /* the child leaves as a scatter request; its stores go out after this trip's table
+             * loads, so no load of the trip waits behind them (vmcnt is in order) */
+            if (F.n_e > 0.0) {
+                push_request(C, L, cold, F, L.p_wc, wstack, wtop);
+                ++children;
             }
+            L.alpha_scatti = a_s;
+            L.alpha_absi = a_a;
+            L.bi = bf;
+            L.tau_abs += L.p_dtau_abs;
+            L.tau_scatt += L.p_dtau_scatt;
+        } else {
+            /* trapezoid optical depths over the step (:957-975) */
             const double dl = L.dl;
             double d_tau_scatt, d_tau_abs, bias;
-            if (bound_flag || nu < 0.0) {
+            if (zero) {
                 d_tau_scatt = 0.5 * L.alpha_scatti * P.d_tau_k * dl;
                 d_tau_abs = 0.5 * L.alpha_absi * P.d_tau_k * dl;
-                L.alpha_scatti = 0.0;
-                L.alpha_absi = 0.0;
                 bias = 0.0;
-                L.bi = 0.0;
             } else {
-                const double a_sf = alpha_inv_scatt(P, nu, F.theta_e, F.n_e);
-                d_tau_scatt = 0.5 * (L.alpha_scatti + a_sf) * P.d_tau_k * dl;
-                L.alpha_scatti = a_sf;
-                const double a_af = alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, theta);
-                d_tau_abs = 0.5 * (L.alpha_absi + a_af) * P.d_tau_k * dl;
-                L.alpha_absi = a_af;
-                const double bf = bias_func(bias_d, F.theta_e, L.w);
+                d_tau_scatt = 0.5 * (L.alpha_scatti + a_s) * P.d_tau_k * dl;
+                d_tau_abs = 0.5 * (L.alpha_absi + a_a) * P.d_tau_k * dl;
                 bias = 0.5 * (L.bi + bf);
-                L.bi = bf;
             }
-            TSTAMP(12);
+            L.alpha_scatti = a_s;
+            L.alpha_absi = a_a;
+            L.bi = bf;
             const double x1 = -log(uniform(L.rng));
             const double wc = L.w / bias;
             if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) {
@@ -636,8 +670,8 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     return true;
 }
 
-/* LDS per lane: photon_2 (13 doubles) + push backup (12 doubles), [slot][lane] */
-constexpr int LDS_DOUBLES_PER_LANE = 25;
+/* LDS per lane: photon_2 (13 doubles), [slot][lane] */
+constexpr int LDS_DOUBLES_PER_LANE = 13;
 
 __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P, Ctl C) {
 #ifdef GRM_TIMING
@@ -646,14 +680,17 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
 #endif
     __shared__ double lds[LDS_DOUBLES_PER_LANE * BLOCK];
     const Slot ph2{lds + threadIdx.x, BLOCK};
-    const Slot bk{lds + 13 * BLOCK + threadIdx.x, BLOCK};
     const unsigned lane_id = threadIdx.x & 63;
     const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const Slot bk{C.bk + gtid, C.lanes};
     const int wave = threadIdx.x >> 6;
     SReq *wstack = C.stack + (gtid >> 6) * WSTACK_CAP;
     __shared__ int s_wtop[BLOCK / 64];
     int *wtop = s_wtop + wave;
     if (lane_id == 0) *wtop = 0;
+    for (int i = threadIdx.x; i < SPEC_LDS; i += BLOCK) s_spec[i] = 0.0;
+    if (lane_id < 4) s_cnt[wave][lane_id] = 0;
+    __syncthreads();
     Cold *cold = C.cold + gtid;
     Lane L;
     L.rng.k0 = C.key0;
@@ -667,8 +704,9 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
 
     while (true) {
         TCOUNT(4);
-        if ((trip++ & 15) == 0 && !C.bias_frozen) {
-            bias_d = bias_den(P, C);
+        if ((trip++ & 15) == 0) {
+            flush_counters(C);
+            if (!C.bias_frozen) bias_d = bias_den(P, C);
             TSTAMP(7);
         }
         /* Batched refill (converged point).  Idle lanes wait until at least refill_min of them can
@@ -745,6 +783,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         for (int r = 0; r < 15; ++r) atomicAdd(C.timing + r, g_tlds[threadIdx.x >> 6][r]);
     }
 #endif
+    /* counters, then the workgroup's spectrum, to the global accumulators */
+    flush_counters(C);
+    __syncthreads();
+    for (int i = threadIdx.x; i < SPEC_LDS; i += BLOCK) {
+        const double v = s_spec[i];
+        if (v != 0.0) unsafeAtomicAdd(reinterpret_cast<double *>(C.spec + i / SPEC_FIELDS) + i % SPEC_FIELDS, v);
+    }
     /* wave-reduce the lane counters, one atomic per wave */
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -776,6 +821,7 @@ struct grm_engine {
     grm_spectrum_cell *d_spec = nullptr;
     SReq *d_stack = nullptr;
     Cold *d_cold = nullptr;
+    double *d_bk = nullptr;
     size_t lanes = 0;
     int grid = 0;
     SReq *d_ovf[2] = {nullptr, nullptr};
@@ -828,10 +874,13 @@ int alloc_lanes(grm_engine *e) {
     if (lanes != e->lanes) {
         if (e->d_stack) (void)hipFree(e->d_stack);
         if (e->d_cold) (void)hipFree(e->d_cold);
+        if (e->d_bk) (void)hipFree(e->d_bk);
         e->d_stack = nullptr;
         e->d_cold = nullptr;
+        e->d_bk = nullptr;
         HIPCHK(e, hipMalloc(&e->d_stack, lanes * STACK_DEPTH * sizeof(SReq)));
         HIPCHK(e, hipMalloc(&e->d_cold, lanes * sizeof(Cold)));
+        HIPCHK(e, hipMalloc(&e->d_bk, lanes * 12 * sizeof(double)));
         e->lanes = lanes;
     }
     e->grid = grid;
@@ -871,6 +920,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     C.trace_count = e->d_small + 3;
     C.timing = e->d_timing;
     C.refill_min = e->refill_min;
+    C.bk = e->d_bk;
+    C.lanes = (int)e->lanes;
     C.bias_frozen = e->bias_mode;
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
@@ -1053,6 +1104,7 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_spec);
     hipFree(e->d_stack);
     hipFree(e->d_cold);
+    hipFree(e->d_bk);
     hipFree(e->d_ovf[0]);
     hipFree(e->d_ovf[1]);
     hipFree(e->d_small);

@@ -23,6 +23,9 @@ print(f"emit {len(ph)} photons {time.time() - t:.2f}s", flush=True)
 e = G.Engine(m, 0)
 if grid:
     e.set_option(G.OPT_GRID_BLOCKS, grid)
+if os.environ.get("WARMUP"):
+    e.set_option(G.OPT_WARMUP, int(os.environ["WARMUP"]))
+    print(f"warmup {os.environ['WARMUP']}", flush=True)
 if os.environ.get("REFILL_MIN"):
     e.set_option(G.OPT_REFILL_MIN, int(os.environ["REFILL_MIN"]))
     print(f"refill_min {os.environ['REFILL_MIN']}", flush=True)
