@@ -7,8 +7,11 @@
 Workload (BASELINE.json configs[1]): dump019 at photon_n = 1e6, mass_unit = 4e19.  dump019 is not
 available offline, so a deterministic synthetic HARM dump of dump019's class (192x192 MKS torus,
 a = 0.9375; cuda-grmonty_amd/grmonty_amd/synth_dump.py) is used -- "data": "synthetic".
-A step = one run_simulation pass: every emitted superphoton (already resident in HBM) is tracked to
-completion (scattered children included), then spectrum + counters are reduced.
+A step = one run_simulation pass (harm_model.cpp:340-414) on the GPU: the superphotons are emitted on
+the device from the zone table already resident in HBM (grm_engine_emit: zone counts, scan,
+sample_zone_photon), every one of them is tracked to completion (scattered children included), then
+spectrum + counters are reduced.  `--host-emit` instead times transport only, over photons emitted
+on the host and uploaded before the timed region (the previous definition of a step).
 
 Multi-GPU (weak scaling): N ranks run ONE job of photon_n x N whose zones are split into N
 contiguous ranges of equal expected photon count; zone emission streams and photon stream ids are
@@ -20,7 +23,8 @@ initialised, because a second HIP runtime in the process cannot open the GPU.  E
 returns after its stream has synchronised, so the barriers bracket finished device work.
 
 value = superphotons emitted by all ranks (the reference's "created", harm_model.cpp:407-409) per
-second of max-over-ranks wall time of the K timed steps.
+second of max-over-ranks wall time of the K timed steps -- the reference's "Final rate" window
+(emission + transport, tables already built).
 """
 from __future__ import annotations
 
@@ -51,8 +55,11 @@ def parse():
     ap.add_argument("--dump", default="", help="HARM dump to use (default: synthetic dump019-class)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--host-emit", action="store_true",
+                    help="emit on the host, upload before timing, time transport only")
     ap.add_argument("--pmc-summary", default=os.environ.get("GRM_PMC_SUMMARY", ""),
-                    help="rocprofv3 --pmc counter CSV (FETCH_SIZE/WRITE_SIZE) to fill roofline.traffic")
+                    help="rocprofv3 --pmc counter CSVs, comma-separated (FETCH_SIZE pass, WRITE_SIZE pass) "
+                         "of this same command, to fill roofline.traffic")
     return ap.parse_args()
 
 
@@ -65,38 +72,59 @@ def host_threads(world: int) -> int:
 
 def cpu_baseline(path: str, photon_n: int, photons: np.ndarray, seconds: float):
     """The oracle (single-thread C++ restatement of the reference CPU path; reference semantics:
-    serial, mt19937, live adaptive bias) on a bounded random sample of the same photons."""
+    serial, mt19937, live adaptive bias) on a bounded random sample of the same photons, plus the
+    oracle's emission (zone walk + sample_zone_photon) timed on a random sample of zones: the CPU
+    cost of one superphoton = emission + transport, as in the reference's run_simulation."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py as O
     m = O.OracleModel(path, photon_n=photon_n)
     m.init(host_threads(1))
-    order = np.random.default_rng(0).permutation(len(photons))
+    rng = np.random.default_rng(0)
+    order = rng.permutation(len(photons))
     done, t0, chunk = 0, time.time(), 256
     while time.time() - t0 < seconds and done < len(order):
         sel = np.ascontiguousarray(photons[order[done:done + chunk]]).view(O.INIT_PHOTON)
         m.track(sel, rng_mode=0, seed=123, frozen=False)
         done += len(sel)
-    dt = time.time() - t0
-    return {"value": done / dt, "unit": "superphotons/s", "cores": 1, "kind": "port",
-            "sample": f"{done} of the {len(photons)} emitted superphotons (random subset) tracked by the oracle "
-                      f"(oracle/grmonty_oracle.cpp: serial reference CPU semantics, mt19937, live bias) in "
-                      f"{dt:.1f} s on 1 host core"}
+    t_track = time.time() - t0
+    h = m.header
+    zones = rng.permutation(h.n[0] * h.n[1])
+    n_em, t0 = 0, time.time()
+    for z in zones:
+        n_em += len(m.emit_philox(seed=123, z0=int(z), z1=int(z) + 1))
+        if time.time() - t0 > max(1.0, 0.1 * seconds):
+            break
+    t_emit = time.time() - t0
+    per = t_track / max(done, 1) + t_emit / max(n_em, 1)
+    return {"value": 1.0 / per, "unit": "superphotons/s", "cores": 1, "kind": "port",
+            "sample": f"{done} of the {len(photons)} emitted superphotons (random subset) tracked in {t_track:.1f} s "
+                      f"+ {n_em} superphotons emitted from random zones in {t_emit:.1f} s by the oracle "
+                      f"(oracle/grmonty_oracle.cpp: serial reference CPU semantics, mt19937, live bias) on 1 "
+                      f"host core"}
 
 
-def pmc_traffic(path: str):
-    """HBM bytes of all track_kernel dispatches in a rocprofv3 --pmc CSV (FETCH_SIZE/WRITE_SIZE in KB;
-    gfx950 FETCH_SIZE reports half of wide streaming reads -> doubled, MI355X_MICROARCH.md §HBM)."""
-    if not path or not os.path.exists(path):
+def pmc_traffic(path: str, k: int):
+    """HBM bytes per dominant track_kernel dispatch from rocprofv3 --pmc counter CSVs (FETCH_SIZE and
+    WRITE_SIZE in KB, from separate passes; gfx950 FETCH_SIZE reports half of wide streaming reads ->
+    doubled, MI355X_MICROARCH.md §HBM).  `path` = comma-separated CSVs; per counter, the mean over the
+    k largest dispatches (one dominant launch per step)."""
+    if not path:
         return None
     import csv
-    tot = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
-    seen = False
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if "track_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") in tot:
-                tot[row["Counter_Name"]] += float(row.get("Counter_Value", 0))
-                seen = True
-    return (2.0 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0 if seen else None
+    per = {"FETCH_SIZE": {}, "WRITE_SIZE": {}}
+    for f in path.split(","):
+        if not os.path.exists(f):
+            return None
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                c = row.get("Counter_Name")
+                if "track_kernel" in row.get("Kernel_Name", "") and c in per:
+                    d = row.get("Dispatch_Id", "0")
+                    per[c][d] = per[c].get(d, 0.0) + float(row.get("Counter_Value", 0))
+    if not per["FETCH_SIZE"] or not per["WRITE_SIZE"]:
+        return None
+    top = {c: sorted(v.values())[-k:] for c, v in per.items()}
+    return (2.0 * np.mean(top["FETCH_SIZE"]) + np.mean(top["WRITE_SIZE"])) * 1024.0
 
 
 def main():
@@ -133,12 +161,21 @@ def main():
         uid = [G.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         engine.comm_init(uid[0], world, rank)
-    d_ph = engine.upload(photons)  # inputs resident in HBM before the timed region
+    # inputs resident in HBM before the timed region: the zone table (device emission) or the
+    # host-emitted photons (--host-emit)
+    engine.emit_setup(model)
+    d_ph = engine.upload(photons) if args.host_emit else None
 
     def step():
         engine.reset()
         engine.set_option(G.OPT_ID_BASE, id_base)
-        engine.track_device(d_ph, n)
+        if args.host_emit:
+            engine.track_device(d_ph, n)
+        else:
+            ptr, n_dev = engine.emit(seed=123, z0=z0, z1=z1)
+            if n_dev != n:
+                raise RuntimeError(f"device emission made {n_dev} superphotons, host count {n}")
+            engine.track_device(ptr, n_dev)
         st = engine.stats()
         if world > 1:
             engine.allreduce()
@@ -150,13 +187,16 @@ def main():
     if dist is not None:
         dist.barrier()
     t0 = time.time()
-    kern_ms, steps_tot, tracked, children = 0.0, 0, 0, 0
+    kern_ms, steps_tot, tracked, children, emit_ms, big_ms, big_steps = 0.0, 0, 0, 0, 0.0, 0.0, 0
     for _ in range(args.steps):
         st, n_rec, n_scatt = step()
         kern_ms += st["last_kernel_ms"]
         steps_tot += st["last_steps"]
         tracked += st["n_tracked"]
         children += st["n_children"]
+        emit_ms += 0.0 if args.host_emit else st["last_emit_ms"]
+        big_ms += st["max_launch_ms"]
+        big_steps += st["max_launch_steps"]
     if dist is not None:
         dist.barrier()
     elapsed = time.time() - t0
@@ -170,8 +210,9 @@ def main():
         tmax, total = float(tm[0]), int(tt[0])
     if rank == 0:
         k_ms = kern_ms / args.steps
-        achieved = steps_tot / args.steps * ALG_BYTES_PER_STEP / (k_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.pmc_summary)
+        # per launch, for the dominant track_kernel launch of each step (rocprof's longest dispatches)
+        achieved = big_steps * ALG_BYTES_PER_STEP / (big_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args.pmc_summary, args.steps + args.warmup)
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             try:
@@ -179,7 +220,8 @@ def main():
             except Exception as ex:  # the baseline is reported beside the product, never part of it
                 cpu = {"value": None, "error": repr(ex)}
         out = {
-            "metric": "superphotons/sec on dump019-class HARM dump (photon_n=1e6 per GPU)",
+            "metric": "superphotons/sec on dump019-class HARM dump (photon_n=1e6 per GPU)"
+                      + (" [transport only]" if args.host_emit else ""),
             "value": total / tmax,
             "unit": "superphotons/s",
             "n_gpus": world,
@@ -198,12 +240,15 @@ def main():
                        "superphotons_rank0": n, "parallelism": f"zone shards x{world}, RCCL spectrum all-reduce"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic / max(1, args.steps + args.warmup) if traffic else None,
-                         "note": f"{ALG_BYTES_PER_STEP} algorithmic B per transport step x {steps_tot // args.steps} "
-                                 f"steps per pass / {k_ms:.1f} ms of track_kernel (HIP events on the engine stream); "
-                                 f"the kernel is fp64-VALU/latency bound -- DESIGN.md"},
+                         "traffic": traffic,
+                         "note": f"dominant track_kernel launch: {ALG_BYTES_PER_STEP} algorithmic B per transport step x "
+                                 f"{big_steps // args.steps} steps / {big_ms / args.steps:.1f} ms (HIP events on the "
+                                 f"engine stream); all launches of a step: {steps_tot // args.steps} steps in "
+                                 f"{k_ms:.1f} ms; the kernel is fp64-VALU/latency bound -- DESIGN.md"},
             "cpu_baseline": cpu,
             "detail": {"transport_steps_per_s": steps_tot / (kern_ms * 1e-3), "kernel_ms_per_step": k_ms,
+                       "emit_ms_per_step": emit_ms / args.steps,
+                       "emission": "host (untimed)" if args.host_emit else "device (timed)",
                        "tracked_per_step": tracked // args.steps, "children_per_step": children // args.steps,
                        "launches_total": launches, "init_s": t_init, "emit_s": t_emit},
         }

@@ -32,15 +32,22 @@
 #include <rccl/rccl.h>
 
 #include "grm_device.h"
+#include "grm_emit.h"
 
 using namespace grm;
 
 namespace {
 
-#ifndef GRM_WAVES_PER_SIMD
-#define GRM_WAVES_PER_SIMD 1
+/* One workgroup per CU (its LDS spectrum fills most of the CU's LDS), BLOCK / 256 waves per SIMD.
+ * 512 lanes (2 waves per SIMD) fit the LDS but not the registers: the kernel holds ~460 VGPR+AGPR
+ * per lane at one wave per SIMD and spills ~0.9 KB per lane at 256. */
+#ifndef GRM_BLOCK
+#define GRM_BLOCK 256
 #endif
-constexpr int BLOCK = 256;
+#ifndef GRM_WAVES_PER_SIMD
+#define GRM_WAVES_PER_SIMD (GRM_BLOCK / 256)
+#endif
+constexpr int BLOCK = GRM_BLOCK;
 constexpr int MIN_WAVES_PER_SIMD = GRM_WAVES_PER_SIMD;
 constexpr int STACK_DEPTH = 16;                 /* scatter-request slots per lane ... */
 constexpr int WSTACK_CAP = 64 * STACK_DEPTH;    /* ... pooled into one stack per wave (208 KB of HBM) */
@@ -71,7 +78,7 @@ static_assert(sizeof(Cold) == 80, "Cold layout");
 struct DevCounters {
     unsigned long long n_recorded, n_scatt, max_tau_bits, n_steps;
     unsigned long long n_tracked, n_children, n_overflow, n_dropped;
-    unsigned long long n_primaries, pad[7];
+    unsigned long long n_primaries, max_nstep, n_long, pad[5];
 };
 
 struct Ctl {
@@ -95,7 +102,7 @@ struct Ctl {
     double f_scatt, f_rec, f_maxtau;
     unsigned long long *timing; /* GRM_TIMING builds: per-region wave cycles */
     int refill_min;             /* idle lanes a wave gathers before it refills (batching) */
-    double *bk;                 /* push backup of the halving walk, [12][lanes] (rarely touched) */
+    unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     int lanes;
 };
 
@@ -111,6 +118,8 @@ struct Lane {
     int phase, depth;
     uint32_t pend;
     double dl, hlen;                      /* step size of this iteration; length being pushed */
+    double ph2_x0, ph2_e0s;               /* photon_2's x^0 and e_0_s (the rest of it is in LDS) */
+    double bk_x0;                         /* x^0 of the halving backup (the rest of it is in LDS) */
     double p_dtau_abs, p_dtau_scatt, p_wc; /* carried across the re-push */
 };
 
@@ -153,7 +162,7 @@ __device__ __forceinline__ double bias_func(double den, double t_e, double w) {
  * 8 phase-0 block, 9 push attempt, 10 restore / halving bookkeeping, 11 fluid gather,
  * 12 radiation + bias, 13 rest of the interaction; 15 = last stamp.  Never built into the product. */
 #ifdef GRM_TIMING
-__shared__ unsigned long long g_tlds[4][16];
+__shared__ unsigned long long g_tlds[GRM_BLOCK / 64][16];
 __device__ __forceinline__ void tstamp(int r) {
     const unsigned long long t = __builtin_amdgcn_s_memtime();
     const unsigned long long ex = __ballot(1);
@@ -477,6 +486,45 @@ __device__ __forceinline__ void push_request(const Ctl &C, const Lane &L, const 
     }
 }
 
+/* Two per-lane state copies live in LDS ([slot][lane], conflict-free 8-B words), 11 slots each:
+ * x^1..x^3, k, dk/dlambda; their x^0 (and photon_2's e_0_s) stay in registers.
+ *   ph2: photon_2 (harm_model.cpp:920-925), also the depth-0 backup of push_photon;
+ *   bk:  the backup of push_photon at depth > 0 (x_cpy/k_cpy/dk_cpy, :1222-1228).
+ * 2 x 11 x 8 B x 256 lanes + the 115 KB spectrum = 160 KB, one CU's LDS: no global memory
+ * traffic on the halving path (a lane deep in halving runs alone at the end of a launch). */
+constexpr int LDS_DOUBLES_PER_LANE = 11;
+
+__device__ __forceinline__ void save_xkdk(const Slot &s, const Lane &L) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) s[i] = L.x[1 + i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        s[3 + i] = L.k[i];
+        s[7 + i] = L.dk[i];
+    }
+}
+
+__device__ __forceinline__ void load_xkdk(const Slot &s, Lane &L) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) L.x[1 + i] = s[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        L.k[i] = s[3 + i];
+        L.dk[i] = s[7 + i];
+    }
+}
+
+__device__ __forceinline__ void store_ph2(const Slot &ph2, Lane &L) {
+    L.ph2_x0 = L.x[0];
+    L.ph2_e0s = L.e_0_s;
+    save_xkdk(ph2, L);
+}
+
+__device__ __forceinline__ void load_ph2(const Slot &ph2, Lane &L) {
+    L.x[0] = L.ph2_x0;
+    load_xkdk(ph2, L);
+}
+
 /* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
  * completed a step, the rest of the while-loop body of track_super_photon
  * (harm_model.cpp:919-1063).  A lane that has to halve its step (push_photon's recursion,
@@ -491,13 +539,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             return false;
         }
         /* photon_2 (:920-925) -- also the depth-0 backup of the push */
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            ph2[i] = L.x[i];
-            ph2[4 + i] = L.k[i];
-            ph2[8 + i] = L.dk[i];
-        }
-        ph2[12] = L.e_0_s;
+        store_ph2(ph2, L);
         L.dl = step_size(P, L.x, L.k);
         L.hlen = L.dl;
         L.depth = 0;
@@ -512,24 +554,19 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     bool have_tg = false;
     if (!(L.x[1] < P.xs1)) {
         if (L.depth > 0) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                bk[i] = L.x[i];
-                bk[4 + i] = L.k[i];
-                bk[8 + i] = L.dk[i];
-            }
+            L.bk_x0 = L.x[0];
+            save_xkdk(bk, L);
         }
         double e_1;
         const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -L.depth), e_1, T, G,
                                        [&](const double *xn) { zone_fetch(P, xn, Z); });
         TSTAMP(9);
         if (fail && L.depth < MAX_SUBDIV) {
-            const Slot &src = L.depth == 0 ? ph2 : bk;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                L.x[i] = src[i];
-                L.k[i] = src[4 + i];
-                L.dk[i] = src[8 + i];
+            if (L.depth == 0) {
+                load_ph2(ph2, L);
+            } else {
+                L.x[0] = L.bk_x0;
+                load_xkdk(bk, L);
             }
             ++L.depth;
             L.pend |= 1u << L.depth;
@@ -631,13 +668,8 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
                 else
                     L.w *= exp(-d_tau);
                 /* re-push photon_2 by dl*frac to the scattering point (:1005), on later trips */
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    L.x[i] = ph2[i];
-                    L.k[i] = ph2[4 + i];
-                    L.dk[i] = ph2[8 + i];
-                }
-                L.e_0_s = ph2[12];
+                load_ph2(ph2, L);
+                L.e_0_s = L.ph2_e0s;
                 L.hlen = dl * frac;
                 L.depth = 0;
                 L.pend = 0;
@@ -670,19 +702,16 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     return true;
 }
 
-/* LDS per lane: photon_2 (13 doubles), [slot][lane] */
-constexpr int LDS_DOUBLES_PER_LANE = 13;
-
 __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P, Ctl C) {
 #ifdef GRM_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) < 16) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
 #endif
-    __shared__ double lds[LDS_DOUBLES_PER_LANE * BLOCK];
+    __shared__ double lds[2 * LDS_DOUBLES_PER_LANE * BLOCK];
     const Slot ph2{lds + threadIdx.x, BLOCK};
+    const Slot bk{lds + LDS_DOUBLES_PER_LANE * BLOCK + threadIdx.x, BLOCK};
     const unsigned lane_id = threadIdx.x & 63;
     const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const Slot bk{C.bk + gtid, C.lanes};
     const int wave = threadIdx.x >> 6;
     SReq *wstack = C.stack + (gtid >> 6) * WSTACK_CAP;
     __shared__ int s_wtop[BLOCK / 64];
@@ -692,6 +721,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     if (lane_id < 4) s_cnt[wave][lane_id] = 0;
     __syncthreads();
     Cold *cold = C.cold + gtid;
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long wave_trips = 0;
     Lane L;
     L.rng.k0 = C.key0;
     L.rng.k1 = C.key1;
@@ -700,9 +731,11 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     double bias_d = bias_den(P, C); /* wave-uniform, refreshed every 16 trips when live */
     unsigned trip = 1;
     unsigned long long steps = 0, tracked = 0, primaries = 0, children = 0;
+    unsigned long long nstep_max = 0, n_long = 0; /* longest photon life; lives > 100k steps */
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
 
     while (true) {
+        ++wave_trips;
         TCOUNT(4);
         if ((trip++ & 15) == 0) {
             flush_counters(C);
@@ -774,7 +807,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             if (pool_done && *wtop == 0) break;
             continue;
         }
-        if (active) active = transport_trip(P, C, L, cold, wstack, wtop, steps, children, ph2, bk, bias_d);
+        if (active) {
+            active = transport_trip(P, C, L, cold, wstack, wtop, steps, children, ph2, bk, bias_d);
+            if (!active) {
+                nstep_max = max(nstep_max, (unsigned long long)L.n_step);
+                n_long += L.n_step > 100000 ? 1 : 0;
+            }
+        }
         TSTAMP(2);
     }
 #ifdef GRM_TIMING
@@ -797,12 +836,21 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         tracked += __shfl_xor(tracked, off);
         primaries += __shfl_xor(primaries, off);
         children += __shfl_xor(children, off);
+        n_long += __shfl_xor(n_long, off);
+        nstep_max = max(nstep_max, (unsigned long long)__shfl_xor(nstep_max, off));
     }
     if (lane_id == 0) {
         atomicAdd(&C.ctr->n_steps, steps);
         atomicAdd(&C.ctr->n_tracked, tracked);
         atomicAdd(&C.ctr->n_primaries, primaries);
         atomicAdd(&C.ctr->n_children, children);
+        if (n_long) atomicAdd(&C.ctr->n_long, n_long);
+        atomicMax(&C.ctr->max_nstep, nstep_max);
+        unsigned long long *wr = C.waves + (gtid >> 6) * 4;
+        wr[0] = rt_start;
+        wr[1] = __builtin_amdgcn_s_memrealtime();
+        wr[2] = wave_trips;
+        wr[3] = tracked;
     }
 }
 
@@ -821,7 +869,6 @@ struct grm_engine {
     grm_spectrum_cell *d_spec = nullptr;
     SReq *d_stack = nullptr;
     Cold *d_cold = nullptr;
-    double *d_bk = nullptr;
     size_t lanes = 0;
     int grid = 0;
     SReq *d_ovf[2] = {nullptr, nullptr};
@@ -846,6 +893,14 @@ struct grm_engine {
     size_t upload_cap = 0;
     ncclComm_t comm = nullptr;
     unsigned long long *d_timing = nullptr;
+    unsigned long long *d_waves = nullptr; /* [lanes / 64][4] per-wave record of the last launch */
+    /* device emission: zone table, emission tables, zone offsets, emitted photons */
+    grm_emit_zone *d_ezones = nullptr;
+    double *d_eweight = nullptr, *d_ef = nullptr;
+    unsigned long long *d_eoff = nullptr;
+    int64_t n_ezones = 0;
+    grm_init_photon *d_emit = nullptr;
+    size_t emit_cap = 0;
     std::string err;
 };
 
@@ -874,13 +929,13 @@ int alloc_lanes(grm_engine *e) {
     if (lanes != e->lanes) {
         if (e->d_stack) (void)hipFree(e->d_stack);
         if (e->d_cold) (void)hipFree(e->d_cold);
-        if (e->d_bk) (void)hipFree(e->d_bk);
         e->d_stack = nullptr;
         e->d_cold = nullptr;
-        e->d_bk = nullptr;
         HIPCHK(e, hipMalloc(&e->d_stack, lanes * STACK_DEPTH * sizeof(SReq)));
         HIPCHK(e, hipMalloc(&e->d_cold, lanes * sizeof(Cold)));
-        HIPCHK(e, hipMalloc(&e->d_bk, lanes * 12 * sizeof(double)));
+        if (e->d_waves) (void)hipFree(e->d_waves);
+        e->d_waves = nullptr;
+        HIPCHK(e, hipMalloc(&e->d_waves, lanes / 64 * 4 * sizeof(unsigned long long)));
         e->lanes = lanes;
     }
     e->grid = grid;
@@ -919,8 +974,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     C.trace_cap = e->trace_cap;
     C.trace_count = e->d_small + 3;
     C.timing = e->d_timing;
+    C.waves = e->d_waves;
     C.refill_min = e->refill_min;
-    C.bk = e->d_bk;
     C.lanes = (int)e->lanes;
     C.bias_frozen = e->bias_mode;
     if (e->bias_mode && e->frozen_set) {
@@ -944,6 +999,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
         steps_before = h.n_steps;
     }
     double ms_total = 0.0;
+    unsigned long long steps_pass = steps_before;
     int src = -1, dst = 0;
     unsigned long long n_pool = n;
     for (int pass = 0; n_pool > 0; ++pass) {
@@ -960,11 +1016,18 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
         unsigned long long cnt = 0;
+        DevCounters hp;
         HIPCHK(e, hipMemcpyAsync(&cnt, C.ovf_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipMemcpyAsync(&hp, e->d_ctr, sizeof(hp), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         float ms = 0.f;
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
         ms_total += ms;
+        if (ms > e->stats.max_launch_ms) { /* the dominant launch of this transport call */
+            e->stats.max_launch_ms = ms;
+            e->stats.max_launch_steps = hp.n_steps - steps_pass;
+        }
+        steps_pass = hp.n_steps;
         e->stats.n_launches++;
         n_pool = std::min(cnt, e->ovf_cap);
         src = dst;
@@ -992,6 +1055,8 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     if (alloc_lanes(e)) return -1;
     e->stats.last_kernel_ms = 0.0;
     e->stats.last_steps = 0;
+    e->stats.max_launch_ms = 0.0;
+    e->stats.max_launch_steps = 0;
     const uint64_t limit = e->warmup < 0 ? (uint64_t)e->lanes : (uint64_t)e->warmup;
     size_t done = 0;
     while (done < n) {
@@ -1104,7 +1169,6 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_spec);
     hipFree(e->d_stack);
     hipFree(e->d_cold);
-    hipFree(e->d_bk);
     hipFree(e->d_ovf[0]);
     hipFree(e->d_ovf[1]);
     hipFree(e->d_small);
@@ -1112,6 +1176,12 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_trace);
     hipFree(e->d_upload);
     hipFree(e->d_timing);
+    hipFree(e->d_waves);
+    hipFree(e->d_ezones);
+    hipFree(e->d_eweight);
+    hipFree(e->d_ef);
+    hipFree(e->d_eoff);
+    hipFree(e->d_emit);
     if (e->comm) ncclCommDestroy(e->comm);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
@@ -1184,6 +1254,8 @@ int grm_engine_finish(grm_engine *e, grm_spectrum_cell *spec, uint64_t *n_rec, u
     e->stats.n_overflow = h.n_overflow;
     e->stats.n_dropped = h.n_dropped;
     e->stats.n_primaries = h.n_primaries;
+    e->stats.max_photon_steps = h.max_nstep;
+    e->stats.n_long_photons = h.n_long;
     return 0;
 }
 
@@ -1235,6 +1307,80 @@ int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm
     return 0;
 }
 
+int grm_engine_emit_setup(grm_engine *e, const grm_emit_zone *zones, int64_t n_zones, const double *weight,
+                          const double *f) {
+    if (!e) return -1;
+    if (!zones || !weight || !f || n_zones != (int64_t)e->P.n1 * e->P.n2) {
+        e->err = "grm_engine_emit_setup: need the zone table of all n1*n2 zones and both emission tables";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    hipFree(e->d_ezones);
+    hipFree(e->d_eweight);
+    hipFree(e->d_ef);
+    hipFree(e->d_eoff);
+    e->d_ezones = nullptr;
+    e->d_eweight = e->d_ef = nullptr;
+    e->d_eoff = nullptr;
+    e->n_ezones = 0;
+    const size_t nt = GRM_N_E_SAMP + 1;
+    HIPCHK(e, hipMalloc(&e->d_ezones, (size_t)n_zones * sizeof(grm_emit_zone)));
+    HIPCHK(e, hipMalloc(&e->d_eweight, nt * sizeof(double)));
+    HIPCHK(e, hipMalloc(&e->d_ef, nt * sizeof(double)));
+    HIPCHK(e, hipMalloc(&e->d_eoff, ((size_t)n_zones + 1) * sizeof(unsigned long long)));
+    HIPCHK(e, hipMemcpy(e->d_ezones, zones, (size_t)n_zones * sizeof(grm_emit_zone), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_eweight, weight, nt * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_ef, f, nt * sizeof(double), hipMemcpyHostToDevice));
+    e->n_ezones = n_zones;
+    return 0;
+}
+
+int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon **dev_out,
+                    uint64_t *n_out) {
+    if (!e || !dev_out || !n_out) return -1;
+    if (!e->d_ezones) {
+        e->err = "grm_engine_emit: no zone table (grm_engine_emit_setup)";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    if (z1 < 0 || z1 > e->n_ezones) z1 = e->n_ezones;
+    if (z0 < 0) z0 = 0;
+    if (z0 > z1) z0 = z1;
+    /* consts.hpp:33-157 emission constants, host libm like the host model's */
+    EmitParams E;
+    E.zones = e->d_ezones;
+    E.weight = e->d_eweight;
+    E.f = e->d_ef;
+    E.l_nu_min = std::log(1.0e9);
+    const double l_nu_max = std::log(1.0e16);
+    E.n_l_n = l_nu_max - E.l_nu_min;
+    E.d_l_nu = (l_nu_max - E.l_nu_min) / GRM_N_E_SAMP;
+    E.jnu_l_min_k = std::log(0.002);
+    E.jnu_d_l_k = std::log(1.0e7 / 0.002) / GRM_N_E_SAMP;
+    E.k0 = (uint32_t)seed;
+    E.k1 = (uint32_t)(seed >> 32);
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+    uint64_t n = 0;
+    if (grm_emit_launch(e->P, E, (uint64_t)z0, (uint64_t)(z1 - z0), e->d_eoff, e->stream, &e->d_emit, &e->emit_cap,
+                        &n, e->err))
+        return -1;
+    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    HIPCHK(e, hipEventSynchronize(e->ev1));
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    e->stats.last_emit_ms = ms;
+    *dev_out = e->d_emit;
+    *n_out = n;
+    return 0;
+}
+
+int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm_init_photon *host_out) {
+    if (!e || (n && (!dev || !host_out))) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (n) HIPCHK(e, hipMemcpy(host_out, dev, n * sizeof(grm_init_photon), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int grm_engine_debug_timing(grm_engine *e, uint64_t out[16], int reset) {
     if (!e || !out) return -1;
     HIPCHK(e, hipSetDevice(e->device));
@@ -1245,6 +1391,16 @@ int grm_engine_debug_timing(grm_engine *e, uint64_t out[16], int reset) {
 #else
     return 0;
 #endif
+}
+
+int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap) {
+    if (!e || !e->d_waves) return -1;
+    if (hipSetDevice(e->device) != hipSuccess) return -1;
+    const size_t n = e->lanes / 64;
+    const size_t k = std::min(n, cap);
+    if (k && out && hipMemcpy(out, e->d_waves, k * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return (int64_t)n;
 }
 
 int grm_rccl_unique_id(uint8_t id_out[128]) {
@@ -1308,6 +1464,7 @@ size_t grm_sizeof(int which) {
     case 3: return sizeof(grm_spectrum_cell);
     case 4: return sizeof(grm_trace);
     case 5: return sizeof(grm_stats);
+    case 6: return sizeof(grm_emit_zone);
     default: return 0;
     }
 }

@@ -6,9 +6,11 @@ fallback: the transport path is the HIP kernel or nothing).
 
     m = Model.load(dump_path, photon_n=1_000_000)     # HARMModel(photon_n, mass_unit).read_file
     m.init(threads)                                     # init(): geometry + tables
-    ph = m.emit(seed=123)                               # emitted superphotons (InitPhoton records)
     e = Engine(m, device=0)                             # cuda_super_photon::alloc_memory
-    e.track(ph)                                         # track_super_photons
+    e.emit_setup(m)                                     # zone table -> HBM
+    ptr, n = e.emit(seed=123)                           # make_super_photon on the GPU
+    e.track_device(ptr, n)                              # track_super_photons
+    (host emission, m.emit(seed) -> InitPhoton records, + e.track(ph) is the same list of photons)
     spec, n_rec, n_scatt, max_tau = e.finish()
     m.write_spectrum(spec, "spectrum.txt")              # report_spectrum
 """
@@ -37,6 +39,10 @@ TRACE = np.dtype([("id", "<u8"), ("parent_id", "<u8"), ("w", "<f8"), ("e", "<f8"
                   ("x3", "<f8"), ("tau_abs", "<f8"), ("tau_scatt", "<f8"), ("n_scatt", "<i4"),
                   ("n_step", "<i4"), ("end_reason", "<i4"), ("ix2", "<i4"), ("i_e", "<i4"), ("pad_", "<i4")])
 
+EMIT_ZONE = np.dtype([("nz", "<f8"), ("dn_max", "<f8"), ("x", "<f8", 4), ("n_e", "<f8"), ("theta_e", "<f8"),
+                      ("b", "<f8"), ("e_con", "<f8", (4, 4)), ("e_cov_t", "<f8", 4), ("e_cov_z", "<f8", 4),
+                      ("pad_", "<f8")])
+
 OPT_SEED, OPT_BIAS_MODE, OPT_TRACE_CAP, OPT_GRID_BLOCKS, OPT_ID_BASE = 0, 1, 2, 3, 4
 OPT_FROZEN_SCATT, OPT_FROZEN_REC, OPT_FROZEN_MAXTAU, OPT_WARMUP, OPT_REFILL_MIN = 5, 6, 7, 8, 9
 N_TH_BINS, N_E_BINS = 6, 200
@@ -60,7 +66,9 @@ class Stats(C.Structure):
     _fields_ = [("n_tracked", C.c_uint64), ("n_primaries", C.c_uint64), ("n_children", C.c_uint64),
                 ("n_steps", C.c_uint64), ("n_overflow", C.c_uint64), ("n_dropped", C.c_uint64),
                 ("n_launches", C.c_uint64), ("kernel_ms", C.c_double), ("last_kernel_ms", C.c_double),
-                ("last_steps", C.c_uint64)]
+                ("last_steps", C.c_uint64), ("last_emit_ms", C.c_double),
+                ("max_launch_ms", C.c_double), ("max_launch_steps", C.c_uint64),
+                ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -93,12 +101,18 @@ SIGNATURES = {
     "grm_model_emit": (C.c_int64, [VP, C.c_uint64, C.c_int64, C.c_int64, VP, C.c_size_t, C.c_int]),
     "grm_model_zone_weights": (C.c_int, [VP, DP]),
     "grm_write_spectrum": (C.c_int, [VP, VP, C.c_char_p, DP]),
+    "grm_model_zone_table": (C.c_int, [VP, C.c_int64, C.c_int64, VP, C.c_int]),
+    "grm_engine_emit_setup": (C.c_int, [VP, VP, C.c_int64, DP, DP]),
+    "grm_engine_emit_setup_from_model": (C.c_int, [VP, VP]),
+    "grm_engine_emit": (C.c_int, [VP, C.c_uint64, C.c_int64, C.c_int64, C.POINTER(VP), C.POINTER(C.c_uint64)]),
+    "grm_engine_download": (C.c_int, [VP, VP, C.c_size_t, VP]),
     "grm_probe": (C.c_int, [VP, C.c_int, DP, C.c_int, DP, C.c_int, C.c_size_t]),
     "grm_engine_upload": (C.c_int, [VP, VP, C.c_size_t, C.POINTER(VP)]),
     "grm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "grm_engine_comm_init": (C.c_int, [VP, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     "grm_engine_allreduce": (C.c_int, [VP]),
     "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
+    "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_sizeof": (C.c_size_t, [C.c_int]),
     "grm_version": (C.c_char_p, []),
 }
@@ -202,6 +216,16 @@ class Model:
             raise RuntimeError(self.L.grm_model_last_error().decode())
         return out
 
+    def zone_table(self, z0: int = 0, z1: int = -1, threads: int = 0) -> np.ndarray:
+        """Per-zone emission records (init_zone nz / dn_max, zone centre, fluid, tetrad)."""
+        h = self.header
+        nz = h.n[0] * h.n[1]
+        z1 = nz if z1 < 0 or z1 > nz else z1
+        out = np.zeros(max(z1 - z0, 0), dtype=EMIT_ZONE)
+        if self.L.grm_model_zone_table(self.h, z0, z1, _ptr(out), threads) != 0:
+            raise RuntimeError(self.L.grm_model_last_error().decode())
+        return out
+
     def zone_weights(self) -> np.ndarray:
         h = self.header
         out = np.zeros(h.n[0] * h.n[1])
@@ -249,6 +273,25 @@ class Engine:
     def set_option(self, opt: int, value: int):
         self._check(self.L.grm_engine_set_option(self.h, opt, int(value)))
 
+    def emit_setup(self, model: "Model"):
+        """Upload the model's zone table and emission tables (once per model)."""
+        rc = self.L.grm_engine_emit_setup_from_model(self.h, model.h)
+        if rc != 0:
+            msg = self.L.grm_engine_last_error(self.h).decode() or self.L.grm_model_last_error().decode()
+            raise RuntimeError(msg)
+
+    def emit(self, seed: int = 123, z0: int = 0, z1: int = -1) -> tuple[int, int]:
+        """Emit the superphotons of zones [z0, z1) on the GPU; returns (device address, count).
+        The buffer is engine-owned and valid until the next emit."""
+        p, n = VP(), C.c_uint64()
+        self._check(self.L.grm_engine_emit(self.h, int(seed), int(z0), int(z1), C.byref(p), C.byref(n)))
+        return int(p.value or 0), int(n.value)
+
+    def download(self, dev_ptr: int, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=INIT_PHOTON)
+        self._check(self.L.grm_engine_download(self.h, C.c_void_p(dev_ptr), int(n), _ptr(out)))
+        return out
+
     def track(self, photons: np.ndarray):
         ph = np.ascontiguousarray(photons, dtype=INIT_PHOTON)
         self._check(self.L.grm_engine_track(self.h, _ptr(ph), len(ph)))
@@ -295,6 +338,16 @@ class Engine:
         out = (C.c_uint64 * 16)()
         instrumented = self.L.grm_engine_debug_timing(self.h, out, 1 if reset else 0)
         return instrumented, list(out)
+
+    def debug_waves(self) -> np.ndarray:
+        """Per-wave record of the last transport launch: (start, exit) s_memrealtime ticks (100 MHz),
+        loop trips, superphotons tracked."""
+        n = self.L.grm_engine_debug_waves(self.h, None, 0)
+        if n < 0:
+            raise RuntimeError("no transport launch yet")
+        out = np.zeros((n, 4), dtype=np.uint64)
+        self.L.grm_engine_debug_waves(self.h, _ptr(out), n)
+        return out
 
     def allreduce(self):
         self._check(self.L.grm_engine_allreduce(self.h))

@@ -112,14 +112,16 @@ struct Philox {
     }
 };
 
-/* emission stream of zone z: counter words 2,3 = (zone, salt 'EMIT') */
-Philox zone_stream(uint64_t seed, uint64_t zone) {
+/* emission streams of zone z: counter words 2,3 = (zone, salt 'EMIT'), word 1 = slot (0 = the
+ * zone's count draw, p + 1 = photon p of the zone), word 0 = draw index.  Photons of one zone are
+ * independent streams, so any lane / thread can sample any photon (the device emitter does). */
+Philox zone_stream(uint64_t seed, uint64_t zone, uint64_t slot = 0) {
     Philox p;
     p.k0 = (uint32_t)seed;
     p.k1 = (uint32_t)(seed >> 32);
     p.c2 = (uint32_t)zone;
     p.c3 = 0x454D4954u ^ (uint32_t)(zone >> 32);
-    p.ctr = 0;
+    p.ctr = slot << 32;
     return p;
 }
 
@@ -482,16 +484,24 @@ double interp_weight(const grm_model *m, double nu) { /* :784-792 */
 }
 
 /* zone's photon count: stochastic rounding with the zone stream's first draw (:693-697) */
-int zone_count(const grm_model *m, uint64_t seed, int i, int j, double &dn_max, Philox &rs) {
-    double nz;
+int zone_count(const grm_model *m, uint64_t seed, int i, int j) {
+    double nz, dn_max;
     zone_budget(m, i, j, nz, dn_max);
-    rs = zone_stream(seed, (uint64_t)i * m->n2() + j);
+    Philox rs = zone_stream(seed, (uint64_t)i * m->n2() + j);
     return (std::fmod(nz, 1.0) > rs.uniform()) ? (int)nz + 1 : (int)nz;
 }
 
-/* sample_zone_photon (harm_model.cpp:706-782) for all photons of one zone */
-void emit_zone(const grm_model *m, int i, int j, int count, double dn_max, Philox &rs, grm_init_photon *out) {
+/* emission record of zone (i,j): init_zone (:1337-1389), the zone centre, get_fluid_zone and the
+ * fluid-frame tetrad that sample_zone_photon builds for a zone's first photon (:717-731) */
+void zone_record(const grm_model *m, int i, int j, grm_emit_zone &r) {
+    std::memset(&r, 0, sizeof(r));
+    zone_budget(m, i, j, r.nz, r.dn_max);
+    zone_coord(m, i, j, r.x);
+    if (!(r.nz > 0.0)) return; /* count is 0 for every seed */
     const Fluid fz = zone_fluid(m, i, j);
+    r.n_e = fz.n_e;
+    r.theta_e = fz.theta_e;
+    r.b = fz.b;
     double bh[4];
     if (fz.b > 0.0) {
         for (int q = 0; q < 4; ++q) bh[q] = fz.b_con[q] * m->units.b_unit / fz.b;
@@ -501,44 +511,54 @@ void emit_zone(const grm_model *m, int i, int j, int count, double dn_max, Philo
     }
     double ec[4][4], el[4][4];
     tetrad(fz.u_con, bh, &m->gcov[((size_t)i * m->n2() + j) * 16], ec, el);
-    double x[4];
-    zone_coord(m, i, j, x);
+    for (int a = 0; a < 4; ++a) {
+        for (int b = 0; b < 4; ++b) r.e_con[a][b] = ec[a][b];
+        r.e_cov_t[a] = el[a][0];
+        r.e_cov_z[a] = el[a][3];
+    }
+}
+
+/* sample_zone_photon (harm_model.cpp:706-782) for photons [0, count) of zone z, photon p from
+ * stream slot p + 1 */
+void emit_zone(const grm_model *m, const grm_emit_zone &r, uint64_t seed, uint64_t z, int count,
+               grm_init_photon *out) {
     for (int p = 0; p < count; ++p) {
+        Philox rs = zone_stream(seed, z, (uint64_t)p + 1);
         grm_init_photon &ph = out[p];
         std::memset(&ph, 0, sizeof(ph));
-        for (int q = 0; q < 4; ++q) ph.x[q] = x[q];
+        for (int q = 0; q < 4; ++q) ph.x[q] = r.x[q];
         double nu, w;
         do {
             nu = std::exp(rs.uniform() * K.n_l_n + K.l_nu_min);
             w = interp_weight(m, nu);
-        } while (rs.uniform() > (f_eval(m, fz.theta_e, fz.b, nu) / (w + 1.0e-100)) / dn_max);
+        } while (rs.uniform() > (f_eval(m, r.theta_e, r.b, nu) / (w + 1.0e-100)) / r.dn_max);
         ph.w = w;
-        const double j_max = synch(m, nu, fz.n_e, fz.theta_e, fz.b, kPi / 2.0);
+        const double j_max = synch(m, nu, r.n_e, r.theta_e, r.b, kPi / 2.0);
         double cos_th, th;
         do {
             cos_th = 2.0 * rs.uniform() - 1.0;
             th = std::acos(cos_th);
-        } while (rs.uniform() > (synch(m, nu, fz.n_e, fz.theta_e, fz.b, th) / j_max));
+        } while (rs.uniform() > (synch(m, nu, r.n_e, r.theta_e, r.b, th) / j_max));
         const double sin_th = std::sqrt(1.0 - cos_th * cos_th);
         const double phi = 2.0 * kPi * rs.uniform();
         const double e = nu * HPL / (ME * CL * CL);
         double kt[4] = {e, e * cos_th, e * sin_th * std::cos(phi), e * sin_th * std::sin(phi)};
         for (int a = 0; a < 4; ++a) {
             ph.k[a] = 0.0;
-            for (int b = 0; b < 4; ++b) ph.k[a] += ec[b][a] * kt[b];
+            for (int b = 0; b < 4; ++b) ph.k[a] += r.e_con[b][a] * kt[b];
         }
         kt[0] *= -1.0;
-        double tmp[4];
-        for (int a = 0; a < 4; ++a) {
-            tmp[a] = 0.0;
-            for (int b = 0; b < 4; ++b) tmp[a] += el[b][a] * kt[b];
+        double t0 = 0.0, t3 = 0.0;
+        for (int b = 0; b < 4; ++b) {
+            t0 += r.e_cov_t[b] * kt[b];
+            t3 += r.e_cov_z[b] * kt[b];
         }
-        ph.e = -tmp[0];
-        ph.e_0 = -tmp[0];
-        ph.l = tmp[3];
-        ph.n_e_0 = fz.n_e;
-        ph.theta_e_0 = fz.theta_e;
-        ph.b_0 = fz.b;
+        ph.e = -t0;
+        ph.e_0 = -t0;
+        ph.l = t3;
+        ph.n_e_0 = r.n_e;
+        ph.theta_e_0 = r.theta_e;
+        ph.b_0 = r.b;
         ph.n_scatt = 0;
     }
 }
@@ -816,13 +836,11 @@ int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_
     if (n_threads < 1) n_threads = default_threads();
     const int64_t n = z1 - z0;
     std::vector<int> cnt((size_t)n);
-    std::vector<double> dmax((size_t)n);
     const int CH = 256;
     parallel_for((int)((n + CH - 1) / CH), n_threads, [&](int c) {
         for (int64_t q = (int64_t)c * CH; q < std::min<int64_t>(n, (int64_t)(c + 1) * CH); ++q) {
             const int64_t z = z0 + q;
-            Philox rs;
-            cnt[(size_t)q] = zone_count(m, seed, (int)(z / m->n2()), (int)(z % m->n2()), dmax[(size_t)q], rs);
+            cnt[(size_t)q] = zone_count(m, seed, (int)(z / m->n2()), (int)(z % m->n2()));
         }
     });
     std::vector<int64_t> off((size_t)n + 1, 0);
@@ -837,14 +855,38 @@ int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_
         for (int64_t q = (int64_t)c * CH; q < std::min<int64_t>(n, (int64_t)(c + 1) * CH); ++q) {
             if (cnt[(size_t)q] == 0) continue;
             const int64_t z = z0 + q;
-            const int i = (int)(z / m->n2()), j = (int)(z % m->n2());
-            double dm;
-            Philox rs;
-            zone_count(m, seed, i, j, dm, rs); /* same stream position as the count pass */
-            emit_zone(m, i, j, cnt[(size_t)q], dm, rs, out + off[(size_t)q]);
+            grm_emit_zone r;
+            zone_record(m, (int)(z / m->n2()), (int)(z % m->n2()), r);
+            emit_zone(m, r, seed, (uint64_t)z, cnt[(size_t)q], out + off[(size_t)q]);
         }
     });
     return total;
+}
+
+int grm_model_zone_table(const grm_model *m, int64_t z0, int64_t z1, grm_emit_zone *out, int n_threads) {
+    if (!m || !m->inited || !out) return set_err("zone table: model not initialised");
+    const int64_t nz = (int64_t)m->n1() * m->n2();
+    if (z1 < 0 || z1 > nz) z1 = nz;
+    if (z0 < 0) z0 = 0;
+    const int64_t n = z1 - z0;
+    if (n <= 0) return 0;
+    const int CH = 256;
+    parallel_for((int)((n + CH - 1) / CH), n_threads, [&](int c) {
+        for (int64_t q = (int64_t)c * CH; q < std::min<int64_t>(n, (int64_t)(c + 1) * CH); ++q) {
+            const int64_t z = z0 + q;
+            zone_record(m, (int)(z / m->n2()), (int)(z % m->n2()), out[q]);
+        }
+    });
+    return 0;
+}
+
+int grm_engine_emit_setup_from_model(grm_engine *e, const grm_model *m) {
+    if (!e) return -1;
+    if (!m || !m->inited) return set_err("emit setup: model not initialised");
+    const int64_t nz = (int64_t)m->n1() * m->n2();
+    std::vector<grm_emit_zone> zt((size_t)nz);
+    if (grm_model_zone_table(m, 0, nz, zt.data(), 0)) return -1;
+    return grm_engine_emit_setup(e, zt.data(), nz, m->weight.data(), m->ftab.data());
 }
 
 /* report_spectrum (harm_model.cpp:416-471, d_omega_func :532-536) */

@@ -110,6 +110,11 @@ typedef struct grm_stats {
     double kernel_ms;          /* summed transport-kernel time (HIP events on the engine stream) */
     double last_kernel_ms;     /* duration of the most recent transport call's kernels */
     uint64_t last_steps;       /* steps in the most recent transport call */
+    double last_emit_ms;       /* duration of the most recent grm_engine_emit (count + scan + sampling) */
+    double max_launch_ms;      /* longest transport launch of the most recent transport call ... */
+    uint64_t max_launch_steps; /* ... and the transport steps it made (per-launch roofline) */
+    uint64_t max_photon_steps; /* longest superphoton life (n_step) since the last reset */
+    uint64_t n_long_photons;   /* superphotons that lived more than 100k steps since the last reset */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
@@ -169,6 +174,11 @@ int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm
  * is instrumented, 0 if not; out[] then stays zero) */
 int grm_engine_debug_timing(grm_engine *e, uint64_t out[16], int reset);
 
+/* diagnostic: per-wave record of the last transport launch, 4 x u64 per wave: start and exit
+ * (s_memrealtime, 100 MHz), loop trips, superphotons tracked.  out holds cap waves; returns the
+ * number of waves of the grid (-1 before the first launch). */
+int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap);
+
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
 /* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */
 int grm_rccl_unique_id(uint8_t id_out[128]);
@@ -197,13 +207,46 @@ const double *grm_model_table(const grm_model *m, int which);
 int grm_engine_create_from_model(const grm_model *m, int device, grm_engine **out);
 
 /* Emission (harm_model.cpp:673-892): zone-parallel, deterministic for a given seed whatever
- * n_threads is (per-zone Philox streams).  Returns photons written (<= cap) or -1 on error.
+ * n_threads is (per-zone count draw, then one Philox stream per photon -- the same streams as
+ * grm_engine_emit).  Returns photons written (<= cap) or -1 on error.
  * Call with out=NULL to only count (exact).  zone range [z0, z1) in row-major zone order
  * (z1 < 0 = all) -- used to shard emission across ranks. */
 int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon *out, size_t cap,
                        int n_threads);
 /* cumulative expected photon count per zone, for balanced zone-range sharding (n1*n2 doubles) */
 int grm_model_zone_weights(const grm_model *m, double *out);
+
+/* --- device emission (harm_model.cpp:673-811, 1337-1389) -------------------------------- */
+/* Per-zone emission record, built once per model on the host: init_zone's expected count and
+ * dn_max, the zone centre (get_coord :1639-1644), get_fluid_zone's n_e / Theta_e / |B| and the
+ * fluid-frame tetrad of sample_zone_photon (:717-731, tetrads.cpp:68-124).  272 B. */
+typedef struct grm_emit_zone {
+    double nz;             /* expected superphotons; 0 = the zone emits nothing */
+    double dn_max;
+    double x[4];
+    double n_e, theta_e, b;
+    double e_con[4][4];    /* tetrad basis vectors e_(b)^mu, row b */
+    double e_cov_t[4];     /* e_cov[b][0], b = 0..3 (photon energy, :773) */
+    double e_cov_z[4];     /* e_cov[b][3], b = 0..3 (angular momentum, :775) */
+    double pad_;
+} grm_emit_zone;
+
+/* zone records [z0, z1) (z1 < 0 = all zones) into out[z1 - z0] */
+int grm_model_zone_table(const grm_model *m, int64_t z0, int64_t z1, grm_emit_zone *out, int n_threads);
+/* upload the zone table (all n1*n2 zones) and the weight / F emission tables (GRM_N_E_SAMP+1 each,
+ * log values as in grm_model_table 3 and 2) to the engine */
+int grm_engine_emit_setup(grm_engine *e, const grm_emit_zone *zones, int64_t n_zones, const double *weight,
+                          const double *f);
+int grm_engine_emit_setup_from_model(grm_engine *e, const grm_model *m);
+/* Emit every superphoton of zones [z0, z1) on the GPU (make_super_photon / sample_zone_photon):
+ * zone counts by stochastic rounding of nz with the zone stream's first draw, then one lane per
+ * photon on its own Philox stream (key = seed, counter = (draw, photon-in-zone + 1, zone, 'EMIT')).
+ * The same photons as grm_model_emit (up to device libm rounding).  *dev_out = engine-owned device
+ * buffer valid until the next emit or destroy; synchronous. */
+int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon **dev_out,
+                    uint64_t *n_out);
+/* device -> host copy of n photons from an engine buffer (tests, writers) */
+int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm_init_photon *host_out);
 
 /* report_spectrum (harm_model.cpp:416-471): 200 rows x 37 columns "%10.5g ".
  * out2 (optional): luminosity, max tau_scatt. */
@@ -215,7 +258,7 @@ int grm_write_spectrum(const grm_model *m, const grm_spectrum_cell *spectrum, co
 int grm_probe(grm_engine *e, int which, const double *in, int in_stride, double *out, int out_stride, size_t n);
 
 /* ABI introspection: sizes of the POD structs (0 header 1 units 2 init_photon 3 spectrum_cell
- * 4 trace 5 stats) */
+ * 4 trace 5 stats 6 emit_zone) */
 size_t grm_sizeof(int which);
 const char *grm_version(void);
 

@@ -1909,6 +1909,45 @@ int64_t grmo_emit(grmo_model *m, uint64_t seed, grmo_init_photon *out, size_t ca
 }
 
 void grmo_init_zone(const grmo_model *m, int i, int j, double out[2]) { init_zone(m, i, j, out[0], out[1]); }
+/* Emission with the product's stream definition (per-photon Philox; grm_model_emit /
+ * grm_engine_emit): the reference's zone walk over zones [z0, z1) in row-major order (get_zone,
+ * harm_model.cpp:673-704), zone z's count by stochastic rounding of init_zone's nz with the first
+ * draw of stream (seed; counter (0, 0, z, 'EMIT' ^ z_hi)), photon p of the zone sampled by
+ * sample_zone_photon (:706-782) from stream (seed; counter (draw, p + 1, z, 'EMIT' ^ z_hi)).
+ * out = NULL counts only.  Returns the number of photons of the range. */
+static Rng emit_stream(uint64_t seed, uint64_t z, uint64_t slot) {
+    Rng r = Rng::philox(seed, ((uint64_t)(0x454D4954u ^ (uint32_t)(z >> 32)) << 32) | (uint32_t)z);
+    r.ctr = slot << 32;
+    return r;
+}
+
+int64_t grmo_emit_philox(grmo_model *m, uint64_t seed, int64_t z0, int64_t z1, grmo_init_photon *out, size_t cap) {
+    const int64_t nz_all = (int64_t)m->n1() * m->n2();
+    if (z1 < 0 || z1 > nz_all) z1 = nz_all;
+    if (z0 < 0) z0 = 0;
+    int64_t k = 0;
+    for (int64_t z = z0; z < z1; ++z) {
+        const int i = (int)(z / m->n2()), j = (int)(z % m->n2());
+        double d_num, dn_max;
+        init_zone(m, i, j, d_num, dn_max);
+        Rng r0 = emit_stream(seed, (uint64_t)z, 0);
+        const int num = (std::fmod(d_num, 1.0) > r0.uniform()) ? (int)d_num + 1 : (int)d_num;
+        grmo_model::Zone zone;
+        zone.x_1 = i;
+        zone.x_2 = j;
+        zone.dn_max = dn_max;
+        zone.num_to_gen = num;
+        zone.first_photon = true;
+        for (int p = 0; p < num; ++p) {
+            Rng r = emit_stream(seed, (uint64_t)z, (uint64_t)p + 1);
+            const grmo_init_photon ph = sample_zone_photon(m, zone, r);
+            if (out && (size_t)k < cap) out[k] = ph;
+            ++k;
+        }
+    }
+    return k;
+}
+
 
 /* harm_model.cpp:340-414 (CPU branch) */
 double grmo_run_simulation(grmo_model *m, uint64_t seed) {

@@ -180,6 +180,10 @@ void grmo_get_counters(const grmo_model *m, uint64_t out[4]);
  * Returns the number emitted; *done = 1 when the zone walk is exhausted. */
 int64_t grmo_emit(grmo_model *m, uint64_t seed, grmo_init_photon *out, size_t cap, int *done);
 void grmo_init_zone(const grmo_model *m, int i, int j, double out[2]); /* nz, dn_max */
+/* Emission with the product's per-photon Philox streams (photon-by-photon check of grm_model_emit
+ * and grm_engine_emit): zones [z0, z1) (z1 < 0 = all), count draw = slot 0 of the zone stream,
+ * photon p = slot p + 1.  out = NULL counts only; returns the number of photons. */
+int64_t grmo_emit_philox(grmo_model *m, uint64_t seed, int64_t z0, int64_t z1, grmo_init_photon *out, size_t cap);
 
 /* ---- whole run, reference CPU semantics (main.cpp:43-53, harm_model.cpp:340-414) ---- */
 /* run_simulation with mt19937(123) shared by emission and transport, live counters. */

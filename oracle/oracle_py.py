@@ -116,6 +116,7 @@ def lib():
             "grmo_get_counters": (None, [vp, U64P]),
             "grmo_emit": (C.c_int64, [vp, C.c_uint64, vp, C.c_size_t, C.POINTER(C.c_int)]),
             "grmo_init_zone": (None, [vp, C.c_int, C.c_int, DP]),
+            "grmo_emit_philox": (C.c_int64, [vp, C.c_uint64, C.c_int64, C.c_int64, vp, C.c_size_t]),
             "grmo_run_simulation": (C.c_double, [vp, C.c_uint64]),
             "grmo_report_spectrum": (C.c_int, [vp, C.c_char_p, DP]),
             "grmo_sizeof": (C.c_size_t, [C.c_int]),
@@ -226,6 +227,19 @@ class OracleModel:
         done = C.c_int(0)
         n = self.L.grmo_emit(self.h, seed, out.ctypes.data_as(C.c_void_p), cap, C.byref(done))
         return out[:n]
+
+    def emit_philox(self, seed: int = 123, z0: int = 0, z1: int = -1) -> np.ndarray:
+        """Emission with the product's per-photon Philox streams (zones [z0, z1))."""
+        n = self.L.grmo_emit_philox(self.h, seed, z0, z1, None, 0)
+        out = np.zeros(n, dtype=INIT_PHOTON)
+        got = self.L.grmo_emit_philox(self.h, seed, z0, z1, out.ctypes.data_as(C.c_void_p), n)
+        assert got == n
+        return out
+
+    def init_zone(self, i: int, j: int):
+        out = np.zeros(2)
+        self.L.grmo_init_zone(self.h, i, j, ptr(out))
+        return out[0], out[1]
 
     def track(self, photons: np.ndarray, rng_mode: int = 1, seed: int = 123, id_base: int = 0, frozen: bool = True,
               scatt0: int = 0, rec0: int = 0, max_tau0: float | None = None, trace_cap: int = 0):

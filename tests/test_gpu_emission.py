@@ -1,0 +1,100 @@
+"""GPU emission (cuda-grmonty_amd/csrc/grm_emit.hip) against the oracle's restatement of the
+reference zone walk + sample_zone_photon (harm_model.cpp:673-811) driven by the same per-photon
+Philox streams (oracle grmo_emit_philox).
+
+Counts are bit-exact: the stochastic rounding of every zone uses the same integer Philox draw and
+the same host-built nz.  Photon fields agree to device-libm rounding (OCML exp/log/pow/acos vs
+glibc, FMA contraction): rtol 1e-10 per field; a photon may differ entirely when a rejection
+test (:739-740, :750-751) flips on a last-bit difference -- bounded below 0.1 % of photons.
+Then end to end: device-emitted photons tracked by the device vs oracle-emitted photons tracked by
+the oracle, photon by photon with the bias frozen (same streams for transport)."""
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ["x", "k", "w", "e", "l", "n_e_0", "theta_e_0", "b_0", "e_0"]
+
+
+def _close(a, b, rtol=1e-10):
+    out = np.ones(len(a), dtype=bool)
+    for f in FIELDS:
+        x, y = a[f], b[f]
+        d = np.abs(x - y) <= rtol * np.maximum(np.abs(x), np.abs(y)) + 1e-300
+        out &= d.reshape(len(a), -1).all(axis=1)
+    return out
+
+
+@pytest.fixture(scope="module")
+def eng(model64):
+    import grmonty_amd as G
+    e = G.Engine(model64, device=0)
+    e.emit_setup(model64)
+    return e
+
+
+def test_device_emission_matches_oracle(eng, oracle64):
+    ptr, n = eng.emit(seed=99)
+    dev = eng.download(ptr, n)
+    po = oracle64.emit_philox(seed=99)
+    assert n == len(po) > 10000
+    np.testing.assert_array_equal(dev["x"], po["x"])          # zone centres: exact
+    np.testing.assert_array_equal(dev["n_e_0"], po["n_e_0"])  # zone fluid: host-built, exact
+    np.testing.assert_array_equal(dev["n_scatt"], 0)
+    ok = _close(dev, po)
+    print(f"device emission: {n} photons, {ok.mean():.6f} agree to 1e-10")
+    assert ok.mean() > 0.999
+    # the few flipped rejections still draw from the same distributions
+    assert abs(np.log(dev["e"]).mean() - np.log(po["e"]).mean()) < 1e-3
+
+
+def test_device_emission_shards(eng, model64):
+    import grmonty_amd as G
+    _, n_all = eng.emit(seed=7)
+    full = eng.download(*eng.emit(seed=7))
+    shards = G.shard_zones(model64.zone_weights(), 3)
+    got = []
+    for a, b in shards:
+        p, n = eng.emit(seed=7, z0=a, z1=b)
+        assert n == model64.count(seed=7, z0=a, z1=b)  # device count == host count, exactly
+        got.append(eng.download(p, n))
+    cat = np.concatenate(got)
+    assert len(cat) == n_all
+    assert cat.tobytes() == full.tobytes()  # same streams whatever the range split
+    p, n = eng.emit(seed=7, z0=5, z1=5)
+    assert n == 0
+
+
+def test_emit_then_track_photon_by_photon(eng, model64, oracle64):
+    """run_simulation on the device (emission + transport, frozen bias) vs the oracle's."""
+    import grmonty_amd as G
+    snap = dict(scatt=200, rec=100, maxtau=2e-3)
+    z1 = 400  # a zone range of ~2-3k photons keeps the oracle in seconds
+    ptr, n = eng.emit(seed=123, z1=z1)
+    po = oracle64.emit_philox(seed=123, z1=z1)
+    assert n == len(po)
+    oracle64.reset()
+    tr_o = oracle64.track(po, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=snap["scatt"],
+                          rec0=snap["rec"], max_tau0=snap["maxtau"], trace_cap=1_000_000)
+    eng.reset()
+    eng.set_option(G.OPT_SEED, 123)
+    eng.set_option(G.OPT_ID_BASE, 0)
+    eng.set_option(G.OPT_BIAS_MODE, 1)
+    eng.set_option(G.OPT_FROZEN_SCATT, snap["scatt"])
+    eng.set_option(G.OPT_FROZEN_REC, snap["rec"])
+    eng.set_option(G.OPT_FROZEN_MAXTAU, struct.unpack("<q", struct.pack("<d", snap["maxtau"]))[0])
+    eng.set_option(G.OPT_TRACE_CAP, 1_000_000)
+    eng.track_device(ptr, n)
+    tr_g = eng.trace(1_000_000)
+    _, n_rec, _, _ = eng.finish()
+    eng.set_option(G.OPT_TRACE_CAP, 0)
+    eng.set_option(G.OPT_BIAS_MODE, 0)
+    go = {int(r["id"]): r for r in tr_o}
+    gg = {int(r["id"]): r for r in tr_g}
+    same = sum(1 for i in go if i in gg and go[i]["end_reason"] == gg[i]["end_reason"]
+               and np.isclose(go[i]["w"], gg[i]["w"], rtol=1e-6))
+    frac = same / max(1, len(go))
+    print(f"emit+track: {n} photons, oracle ends {len(go)}, device ends {len(gg)}, agreement {frac:.4f}")
+    assert frac > 0.95

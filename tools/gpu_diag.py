@@ -29,17 +29,38 @@ if os.environ.get("WARMUP"):
 if os.environ.get("REFILL_MIN"):
     e.set_option(G.OPT_REFILL_MIN, int(os.environ["REFILL_MIN"]))
     print(f"refill_min {os.environ['REFILL_MIN']}", flush=True)
+dev_emit = os.environ.get("DEV_EMIT")
+if dev_emit:
+    e.emit_setup(m)
 for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
     e.reset()
+    if os.environ.get("IDB"):
+        e.set_option(G.OPT_ID_BASE, int(os.environ["IDB"].split(",")[rep]))
+    if os.environ.get("SEED"):
+        e.set_option(G.OPT_SEED, int(os.environ["SEED"]) + rep)
     t = time.time()
-    e.track(ph)
+    if dev_emit:
+        p, n_dev = e.emit(seed=123)
+        e.track_device(p, n_dev)
+    else:
+        e.track(ph)
     wall = time.time() - t
     spec, nr, ns, mt = e.finish()
     st = e.stats()
     print(f"rep {rep}: wall {wall:.3f}s kernel {st['last_kernel_ms']:.1f}ms steps {st['last_steps']} "
           f"({st['last_steps'] / st['last_kernel_ms'] / 1e3:.3g} Msteps/s) tracked {st['n_tracked']} "
           f"children {st['n_children']} overflow {st['n_overflow']} launches {st['n_launches']} "
-          f"rate {len(ph) / (st['last_kernel_ms'] * 1e-3):.4g} ph/s rec {nr} scatt {ns}", flush=True)
+          f"rate {len(ph) / (st['last_kernel_ms'] * 1e-3):.4g} ph/s rec {nr} scatt {ns} | longest launch "
+          f"{st['max_launch_ms']:.1f}ms ({st['max_launch_steps']} steps) longest life {st['max_photon_steps']} steps, "
+          f"{st['n_long_photons']} lives > 1e5 steps", flush=True)
+    wv = e.debug_waves().astype(np.float64)
+    t0w = wv[:, 0].min()
+    ex = (wv[:, 1] - t0w) / 1e5  # ms
+    st_ = (wv[:, 0] - t0w) / 1e5
+    q = np.percentile(ex, [0, 10, 50, 90, 99, 100])
+    print(f"  waves {len(wv)}: start max {st_.max():.2f}ms, exit ms p0/10/50/90/99/100 "
+          + "/".join(f"{v:.0f}" for v in q) + f", trips max/median {wv[:, 2].max():.0f}/{np.median(wv[:, 2]):.0f}, "
+          f"photons max/median {wv[:, 3].max():.0f}/{np.median(wv[:, 3]):.0f}", flush=True)
     inst, tm = e.debug_timing(reset=True)
     if inst:
         tot = max(tm[3], 1)
