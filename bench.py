@@ -13,6 +13,13 @@ sample_zone_photon), every one of them is tracked to completion (scattered child
 spectrum + counters are reduced.  `--host-emit` instead times transport only, over photons emitted
 on the host and uploaded before the timed region (the previous definition of a step).
 
+Passes in flight (--jobs, default 4): each pass runs on its own engine (stream, buffers, spectrum,
+counters, bias state) from its own host thread.  A pass ends with a few long-lived superphotons
+(polar Zeno-stepping or full-depth step halving, up to ~1e6 serial push attempts, one lane on one
+CU); the next passes' photons fill the other CUs meanwhile.  Every pass is complete; value is the
+sustained rate of back-to-back passes, and detail.single_pass_rate / pass_latency_s report one pass
+alone.
+
 Multi-GPU (weak scaling): N ranks run ONE job of photon_n x N whose zones are split into N
 contiguous ranges of equal expected photon count; zone emission streams and photon stream ids are
 global, so the union of the shards is exactly the single-GPU job's photon list.  The only exchange
@@ -48,13 +55,15 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--photon-n", type=float, default=1e6, help="photon_n per GPU")
     ap.add_argument("--grid", type=int, default=192)
     ap.add_argument("--dump", default="", help="HARM dump to use (default: synthetic dump019-class)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--jobs", type=int, default=8,
+                    help="run_simulation passes in flight per GPU (engines with their own streams and buffers)")
     ap.add_argument("--host-emit", action="store_true",
                     help="emit on the host, upload before timing, time transport only")
     ap.add_argument("--pmc-summary", default=os.environ.get("GRM_PMC_SUMMARY", ""),
@@ -129,6 +138,10 @@ def pmc_traffic(path: str, k: int):
 
 def main():
     args = parse()
+    # one hardware queue per engine (+1): a pass's long-lived last photons keep its kernel running on
+    # a CU or two, and a kernel queued behind it on a shared hardware queue would wait for it.  HIP
+    # reads this when its runtime starts (the first engine call below); 4 is the box default.
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(4, args.jobs + 1)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -155,22 +168,50 @@ def main():
     n = len(photons)
     assert n == counts[rank]
     id_base = int(sum(counts[:rank]))
-    engine = G.Engine(model, device=local)
-    engine.set_option(G.OPT_SEED, 123)
-    if world > 1:
-        uid = [G.rccl_unique_id() if rank == 0 else None]
+    # HBM per engine: the emitted batch (128 B per superphoton) + two overflow pools (2 x n/4 x 208 B)
+    # + lane stacks; keep the engines of one GPU within ~200 GB of its 288 GB
+    per_engine = n * (128 + 104) + 0.5e9
+    jobs = max(1, min(args.jobs, int(200e9 // per_engine)))
+    engines = [G.Engine(model, device=local) for _ in range(jobs)]
+    for engine in engines:
+        engine.set_option(G.OPT_SEED, 123)
+    if world > 1:  # one RCCL communicator per concurrent pass; pass s uses engine s % jobs on every rank
+        uid = [[G.rccl_unique_id() for _ in range(jobs)] if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        engine.comm_init(uid[0], world, rank)
+        for engine, u in zip(engines, uid[0]):
+            engine.comm_init(u, world, rank)
     # inputs resident in HBM before the timed region: the zone table (device emission) or the
     # host-emitted photons (--host-emit)
-    engine.emit_setup(model)
-    d_ph = engine.upload(photons) if args.host_emit else None
+    for engine in engines:
+        engine.emit_setup(model)
+    d_ph = [engine.upload(photons) for engine in engines] if args.host_emit else None
 
-    def step():
+    import threading
+    ar_turn = [0]
+    ar_cv = threading.Condition()
+    AR_ABORT = 1 << 60
+
+    def allreduce_in_order(engine, s_):
+        """every rank issues pass s_'s collective after passes < s_ (one global order for RCCL)"""
+        with ar_cv:
+            ar_cv.wait_for(lambda: ar_turn[0] == s_ or ar_turn[0] >= AR_ABORT)
+            if ar_turn[0] >= AR_ABORT:
+                raise RuntimeError("another pass failed")
+        try:
+            engine.allreduce()
+        finally:
+            with ar_cv:
+                ar_turn[0] += 1
+                ar_cv.notify_all()
+
+    def step(j, s_):
+        """one run_simulation pass on engine j (its own stream, buffers, spectrum and counters)"""
+        engine = engines[j]
+        t = time.time()
         engine.reset()
         engine.set_option(G.OPT_ID_BASE, id_base)
         if args.host_emit:
-            engine.track_device(d_ph, n)
+            engine.track_device(d_ph[j], n)
         else:
             ptr, n_dev = engine.emit(seed=123, z0=z0, z1=z1)
             if n_dev != n:
@@ -178,29 +219,54 @@ def main():
             engine.track_device(ptr, n_dev)
         st = engine.stats()
         if world > 1:
-            engine.allreduce()
+            allreduce_in_order(engine, s_)
         spec, n_rec, n_scatt, max_tau = engine.finish()
-        return st, n_rec, n_scatt
+        return st, n_rec, n_scatt, time.time() - t
 
-    for _ in range(args.warmup):
-        step()
+    def run(n_steps):
+        """n_steps passes, pass s on engine s % jobs; the engines' host threads run concurrently, so a
+        pass's last long-lived superphoton (one lane on one CU) overlaps the next passes' work"""
+        res = [None] * n_steps
+        err = []
+        ar_turn[0] = 0
+
+        def worker(j):
+            try:
+                for s_ in range(j, n_steps, jobs):
+                    res[s_] = step(j, s_)
+            except Exception as ex:  # surfaced below
+                err.append(ex)
+                with ar_cv:  # do not leave the other threads waiting for this pass's collective
+                    ar_turn[0] = AR_ABORT
+                    ar_cv.notify_all()
+
+        th = [threading.Thread(target=worker, args=(j,)) for j in range(min(jobs, n_steps))]
+        for t_ in th:
+            t_.start()
+        for t_ in th:
+            t_.join()
+        if err:
+            raise err[0]
+        return res
+
+    run(max(args.warmup, jobs))  # every engine warmed (buffers sized, code loaded)
     if dist is not None:
         dist.barrier()
     t0 = time.time()
-    kern_ms, steps_tot, tracked, children, emit_ms, big_ms, big_steps = 0.0, 0, 0, 0, 0.0, 0.0, 0
-    for _ in range(args.steps):
-        st, n_rec, n_scatt = step()
-        kern_ms += st["last_kernel_ms"]
-        steps_tot += st["last_steps"]
-        tracked += st["n_tracked"]
-        children += st["n_children"]
-        emit_ms += 0.0 if args.host_emit else st["last_emit_ms"]
-        big_ms += st["max_launch_ms"]
-        big_steps += st["max_launch_steps"]
+    res = run(args.steps)
     if dist is not None:
         dist.barrier()
     elapsed = time.time() - t0
-    launches = engine.stats()["n_launches"]
+    kern_ms = sum(r[0]["last_kernel_ms"] for r in res)
+    steps_tot = sum(r[0]["last_steps"] for r in res)
+    tracked = sum(r[0]["n_tracked"] for r in res)
+    children = sum(r[0]["n_children"] for r in res)
+    emit_ms = 0.0 if args.host_emit else sum(r[0]["last_emit_ms"] for r in res)
+    big_ms = sum(r[0]["max_launch_ms"] for r in res)
+    big_steps = sum(r[0]["max_launch_steps"] for r in res)
+    pass_s = sorted(r[3] for r in res)
+    longest_life = max(r[0]["max_photon_steps"] for r in res)
+    launches = sum(e_.stats()["n_launches"] for e_ in engines)
     tmax, total = elapsed, n * args.steps
     if dist is not None:
         tm = torch.tensor([elapsed], dtype=torch.float64)
@@ -212,7 +278,7 @@ def main():
         k_ms = kern_ms / args.steps
         # per launch, for the dominant track_kernel launch of each step (rocprof's longest dispatches)
         achieved = big_steps * ALG_BYTES_PER_STEP / (big_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.pmc_summary, args.steps + args.warmup)
+        traffic = pmc_traffic(args.pmc_summary, args.steps + max(args.warmup, jobs))
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             try:
@@ -243,10 +309,16 @@ def main():
                          "traffic": traffic,
                          "note": f"dominant track_kernel launch: {ALG_BYTES_PER_STEP} algorithmic B per transport step x "
                                  f"{big_steps // args.steps} steps / {big_ms / args.steps:.1f} ms (HIP events on the "
-                                 f"engine stream); all launches of a step: {steps_tot // args.steps} steps in "
-                                 f"{k_ms:.1f} ms; the kernel is fp64-VALU/latency bound -- DESIGN.md"},
+                                 f"engine stream, {jobs} passes in flight); all launches of a step: "
+                                 f"{steps_tot // args.steps} steps in {k_ms:.1f} ms; sustained over the timed window "
+                                 f"{steps_tot * ALG_BYTES_PER_STEP / tmax / 1e9:.0f} GB/s; the kernel is "
+                                 f"fp64-VALU/latency bound -- DESIGN.md"},
             "cpu_baseline": cpu,
             "detail": {"transport_steps_per_s": steps_tot / (kern_ms * 1e-3), "kernel_ms_per_step": k_ms,
+                       "passes_in_flight": jobs,
+                       "pass_latency_s": {"min": pass_s[0], "median": pass_s[len(pass_s) // 2], "max": pass_s[-1]},
+                       "single_pass_rate": n / pass_s[len(pass_s) // 2],
+                       "longest_photon_life_steps": longest_life,
                        "emit_ms_per_step": emit_ms / args.steps,
                        "emission": "host (untimed)" if args.host_emit else "device (timed)",
                        "tracked_per_step": tracked // args.steps, "children_per_step": children // args.steps,

@@ -102,6 +102,13 @@ struct Ctl {
     double f_scatt, f_rec, f_maxtau;
     unsigned long long *timing; /* GRM_TIMING builds: per-region wave cycles */
     int refill_min;             /* idle lanes a wave gathers before it refills (batching) */
+    /* Live-bias warm-up inside the launch: the first admit_n pool photons go in batches, each
+     * admitted only when everything started before it (children included) has ended, and as large
+     * as the history behind it (64, 64, 128, 256, ...): bias_func's running counters then evolve as
+     * in the serial reference (harm_model.cpp:1391-1404).  *admit_end = end of the admitted batch
+     * (~0 = no limit), *in_flight = photons started and not ended (children counted when pushed). */
+    unsigned long long admit_n, admit_h0, admit_lim;
+    unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     int lanes;
 };
@@ -112,6 +119,7 @@ struct Lane {
     double w, e_0_s, tau_abs, tau_scatt;
     double alpha_scatti, alpha_absi, bi, fl_ne;
     int n_scatt, n_step;
+    int flight;                           /* warm-up: photons started (+) / ended (-) since the last flush */
     Rng rng;
     /* per-trip push state machine: phase 0 = loop top, 1 = geodesic step in progress,
      * 2 = re-push to the scattering point in progress; depth/pend = position in the halving tree */
@@ -451,8 +459,8 @@ __device__ __forceinline__ void store_sreq(SReq *dst, const SReq &R) {
 }
 
 /* push the scattered photon's child out as a scatter request: onto the wave's stack (HBM entries,
- * top counter in LDS), else the overflow pool */
-__device__ __forceinline__ void push_request(const Ctl &C, const Lane &L, const Cold *cold, const Fluid &F, double wc,
+ * top counter in LDS), else the overflow pool (tracked by the next launch).  true = on the stack */
+__device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const Cold *cold, const Fluid &F, double wc,
                                              SReq *wstack, int *wtop) {
     SReq R;
 #pragma unroll
@@ -476,6 +484,7 @@ __device__ __forceinline__ void push_request(const Ctl &C, const Lane &L, const 
     const int slot = atomicAdd(wtop, 1); /* LDS; values past the cap are clamped at the next refill */
     if (slot < WSTACK_CAP) {
         store_sreq(wstack + slot, R);
+        return true;
     } else {
         const unsigned long long o = atomicAdd(C.ovf_count, 1ull);
         if (o < C.ovf_cap)
@@ -483,6 +492,7 @@ __device__ __forceinline__ void push_request(const Ctl &C, const Lane &L, const 
         else
             atomicAdd(&C.ctr->n_dropped, 1ull);
         atomicAdd(&C.ctr->n_overflow, 1ull);
+        return false;
     }
 }
 
@@ -493,6 +503,7 @@ __device__ __forceinline__ void push_request(const Ctl &C, const Lane &L, const 
  * 2 x 11 x 8 B x 256 lanes + the 115 KB spectrum = 160 KB, one CU's LDS: no global memory
  * traffic on the halving path (a lane deep in halving runs alone at the end of a launch). */
 constexpr int LDS_DOUBLES_PER_LANE = 11;
+constexpr int WARM_GRID = 64; /* workgroups of the warm-up launch (batches of <= lanes/2 photons) */
 
 __device__ __forceinline__ void save_xkdk(const Slot &s, const Lane &L) {
 #pragma unroll
@@ -628,7 +639,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             /* the child leaves as a scatter request; its stores go out after this trip's table
              * loads, so no load of the trip waits behind them (vmcnt is in order) */
             if (F.n_e > 0.0) {
-                push_request(C, L, cold, F, L.p_wc, wstack, wtop);
+                if (push_request(C, L, cold, F, L.p_wc, wstack, wtop)) ++L.flight;
                 ++children;
             }
             L.alpha_scatti = a_s;
@@ -727,7 +738,10 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     L.rng.k0 = C.key0;
     L.rng.k1 = C.key1;
     bool active = false;
-    bool pool_done = false; /* wave-uniform */
+    bool pool_done = false;      /* wave-uniform */
+    bool warm = C.admit_n != 0;  /* wave-uniform: warm-up admission in force */
+    unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
+    L.flight = 0;
     double bias_d = bias_den(P, C); /* wave-uniform, refreshed every 16 trips when live */
     unsigned trip = 1;
     unsigned long long steps = 0, tracked = 0, primaries = 0, children = 0;
@@ -737,7 +751,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     while (true) {
         ++wave_trips;
         TCOUNT(4);
-        if ((trip++ & 15) == 0) {
+        if ((trip++ & 15) == 0 || warm) {
             flush_counters(C);
             if (!C.bias_frozen) bias_d = bias_den(P, C);
             TSTAMP(7);
@@ -754,15 +768,57 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             if (top > WSTACK_CAP) top = WSTACK_CAP;
             const int n_idle = __popcll(idle);
             const int k_child = n_idle < top ? n_idle : top;
-            const int k_pool = pool_done ? 0 : n_idle - k_child;
+            int k_pool = pool_done ? 0 : n_idle - k_child;
             const bool none_active = idle == __ballot(1);
             if (k_child + k_pool >= C.refill_min || none_active || (pool_done && top > 0 && top <= n_idle)) {
                 const int r = __popcll(idle & lt_mask);
                 unsigned long long base = 0;
                 if (k_pool > 0) {
-                    if (lane_id == 0) base = atomicAdd(C.pool_head, (unsigned long long)k_pool);
-                    base = __shfl(base, 0);
-                    if (base + k_pool >= C.n_pool) pool_done = true;
+                    if (warm) {
+                        /* warm-up: claim only inside the admitted batch (CAS); once it is claimed and
+                         * nothing is in flight, one wave admits the next batch */
+                        long long got = 0;
+                        int off = 0;
+                        if (lane_id == 0) {
+                            const unsigned long long end =
+                                __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (end == ~0ull) {
+                                off = 1;
+                            } else {
+                                const unsigned long long head =
+                                    __hip_atomic_load(C.pool_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                base = head;
+                                if (head < end) {
+                                    const unsigned long long want = min((unsigned long long)k_pool, end - head);
+                                    atomicAdd(C.in_flight, want); /* before the claim is visible */
+                                    if (atomicCAS(C.pool_head, head, head + want) == head)
+                                        got = (long long)want;
+                                    else
+                                        atomicAdd(C.in_flight, (unsigned long long)(-(long long)want));
+                                } else if (__hip_atomic_load(C.in_flight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                           0) {
+                                    const unsigned long long h = C.admit_h0 + end;
+                                    const unsigned long long next =
+                                        end >= C.admit_n ? ~0ull
+                                                         : min(C.admit_n, end + max(64ull, min(h, C.admit_lim - h)));
+                                    atomicCAS(C.admit_end, end, next);
+                                }
+                            }
+                        }
+                        if (__shfl(off, 0)) {
+                            warm = false; /* admission over: plain claims from here on */
+                            if (lane_id == 0) base = atomicAdd(C.pool_head, (unsigned long long)k_pool);
+                            base = __shfl(base, 0);
+                        } else {
+                            base = __shfl(base, 0);
+                            k_pool = (int)__shfl(got, 0);
+                        }
+                        if (k_pool > 0 && base + k_pool >= C.n_pool) pool_done = true;
+                    } else {
+                        if (lane_id == 0) base = atomicAdd(C.pool_head, (unsigned long long)k_pool);
+                        base = __shfl(base, 0);
+                        if (base + k_pool >= C.n_pool) pool_done = true;
+                    }
                 }
                 if (lane_id == 0) *wtop = top - k_child;
 #ifdef GRM_TIMING
@@ -779,7 +835,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                     has = true;
                 }
                 TSTAMP(0);
-                if (!active && r >= k_child && k_pool > 0) {
+                if (!active && r >= k_child && r - k_child < k_pool) {
                     const unsigned long long idx = base + (unsigned long long)(r - k_child);
                     if (idx < C.n_pool) {
                         if (C.pool_kind == 0) {
@@ -799,20 +855,44 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 if (has) {
                     ++tracked;
                     if (ok) active = init_photon(P, C, cold, L, bias_d);
+                    if (!active) --L.flight; /* started and ended at once (invalid) */
                 }
                 TSTAMP(1);
             }
         }
         if (!__any(active)) {
+            if (warm) {
+                int d = L.flight; /* flush before waiting: the barrier needs everyone's ends */
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+                if (lane_id == 0 && d) atomicAdd(C.in_flight, (unsigned long long)(long long)d);
+                L.flight = 0;
+            }
             if (pool_done && *wtop == 0) break;
+            if (warm) {
+                /* waiting for the next batch; a barrier that never opens (it cannot, short of a
+                 * counting bug) must not hang the GPU: after ~1 s give the warm-up up for all */
+                if (++wait_trips > (1u << 21) && lane_id == 0)
+                    __hip_atomic_store(C.admit_end, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_s_sleep(16);
+            }
             continue;
         }
+        wait_trips = 0;
         if (active) {
             active = transport_trip(P, C, L, cold, wstack, wtop, steps, children, ph2, bk, bias_d);
             if (!active) {
                 nstep_max = max(nstep_max, (unsigned long long)L.n_step);
                 n_long += L.n_step > 100000 ? 1 : 0;
+                --L.flight;
             }
+        }
+        if (warm) {
+            int d = L.flight;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+            if (lane_id == 0 && d) atomicAdd(C.in_flight, (unsigned long long)(long long)d);
+            L.flight = 0;
         }
         TSTAMP(2);
     }
@@ -873,7 +953,9 @@ struct grm_engine {
     int grid = 0;
     SReq *d_ovf[2] = {nullptr, nullptr};
     unsigned long long ovf_cap = 0;
-    unsigned long long *d_small = nullptr; /* [0] pool head, [1..2] ovf counts, [3] trace count */
+    unsigned long long *d_small = nullptr; /* [0] pool head, [1..2] ovf counts, [3] trace count,
+                                              [4] warm-up in flight, [5] warm-up admitted end */
+    unsigned long long h_small[2] = {0, 0};
     grm_init_photon *d_batch = nullptr;
     size_t batch_cap = 0;
     grm_trace *d_trace = nullptr;
@@ -953,7 +1035,7 @@ int ensure_ovf(grm_engine *e, unsigned long long cap) {
     return 0;
 }
 
-int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
+int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid) {
     if (n == 0) return 0;
     /* overflow pool: children rarely spill (8-deep lane stacks); size ~ max(1M, n/4) */
     if (ensure_ovf(e, std::max<unsigned long long>(1ull << 20, n / 4))) return -1;
@@ -978,6 +1060,16 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     C.refill_min = e->refill_min;
     C.lanes = (int)e->lanes;
     C.bias_frozen = e->bias_mode;
+    C.in_flight = e->d_small + 4;
+    C.admit_end = e->d_small + 5;
+    {
+        /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
+         * counters' history doubles, as the serial reference's bias_func sees them */
+        const uint64_t limit = e->warmup < 0 ? (uint64_t)e->lanes : (uint64_t)e->warmup;
+        C.admit_n = (!e->bias_mode && e->history < limit) ? std::min<uint64_t>(n, limit - e->history) : 0;
+        C.admit_h0 = e->history;
+        C.admit_lim = limit;
+    }
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
         C.f_rec = e->fz_rec;
@@ -1004,15 +1096,24 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     unsigned long long n_pool = n;
     for (int pass = 0; n_pool > 0; ++pass) {
         HIPCHK(e, hipMemsetAsync(e->d_small, 0, 3 * sizeof(unsigned long long), e->stream));
+        if (pass == 0 && C.admit_n) { /* [4] in flight = 0, [5] end of the first warm-up batch */
+            const unsigned long long h = C.admit_h0;
+            e->h_small[0] = 0;
+            e->h_small[1] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
+                                                                        64ull, std::min(h, C.admit_lim - h)));
+            HIPCHK(e, hipMemcpyAsync(e->d_small + 4, e->h_small, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice,
+                                     e->stream));
+        }
         C.ovf = e->d_ovf[dst];
         C.ovf_count = e->d_small + 1 + dst;
         if (pass > 0) {
             C.pool = e->d_ovf[src];
             C.pool_kind = 1;
             C.n_pool = n_pool;
+            C.admit_n = 0;
         }
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-        hipLaunchKernelGGL(track_kernel, dim3(e->grid), dim3(BLOCK), 0, e->stream, e->P, C);
+        hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
         unsigned long long cnt = 0;
@@ -1047,26 +1148,26 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     return 0;
 }
 
-/* one transport call: with live bias, the first photons after a reset go in launches that
- * double the tracked history (64, 64, 128, ...) so that the adaptive bias of
- * harm_model.cpp:1391-1404 sees counters close to the serial reference's; afterwards a single
- * persistent launch updates them live. */
+/* one transport call = one persistent launch (+ overflow relaunches); the live-bias warm-up is
+ * admission control inside the launch (Ctl.admit_n) */
 int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     if (alloc_lanes(e)) return -1;
     e->stats.last_kernel_ms = 0.0;
     e->stats.last_steps = 0;
     e->stats.max_launch_ms = 0.0;
     e->stats.max_launch_steps = 0;
+    /* the live-bias warm-up (admission batches, mostly idle lanes waiting for a batch to finish) runs
+     * as its own launch on a small grid, so its CUs stay free for other work on the device (e.g. the
+     * next pass's engine); then the rest on the full grid */
     const uint64_t limit = e->warmup < 0 ? (uint64_t)e->lanes : (uint64_t)e->warmup;
-    size_t done = 0;
-    while (done < n) {
-        size_t sub = n - done;
-        if (!e->bias_mode && e->history < limit)
-            sub = std::min<size_t>(sub, std::max<uint64_t>(64, std::min<uint64_t>(e->history, limit - e->history)));
-        if (run_passes(e, d_batch + done, sub)) return -1;
-        done += sub;
+    if (!e->bias_mode && e->history < limit && n > 0) {
+        const size_t w = (size_t)std::min<uint64_t>(n, limit - e->history);
+        const int grid_w = std::min(e->grid, WARM_GRID);
+        if (run_passes(e, d_batch, w, grid_w)) return -1;
+        d_batch += w;
+        n -= w;
     }
-    return 0;
+    return run_passes(e, d_batch, n, e->grid);
 }
 
 int reset_counters(grm_engine *e) {
