@@ -4,10 +4,10 @@
  *
  *   grmonty_amd --harm_dump_path=DUMP --spectrum_path=OUT [--photon_n=5000000]
  *               [--mass_unit=4e19] [--verbosity=info] [--device=0] [--seed=123]
- *               [--batch=4194304] [--threads=0]
+ *               [--batch=67108864] [--threads=0] [--host_emit]
  *
- * read_file -> init -> run_simulation (emission on host threads, transport on the GPU, in
- * batches; emission of batch b+1 overlaps transport of batch b) -> report_spectrum.
+ * read_file -> init -> run_simulation (zone batches emitted and tracked on the GPU; --host_emit:
+ * emitted on host threads, batch b+1 overlapping the transport of batch b) -> report_spectrum.
  * "Final rate" = created superphotons / wall time of run_simulation, as in the reference.
  */
 #include <chrono>
@@ -56,7 +56,8 @@ int main(int argc, char **argv) {
     std::string dump, spec_path, verbosity = "info";
     int device = 0, threads = 0;
     unsigned long long seed = 123; /* consts.hpp:14 */
-    long long batch = 1ll << 22;
+    long long batch = 1ll << 26; /* photons per zone batch (8.6 GB of emitted photons) */
+    bool host_emit = false;
     for (int i = 1; i < argc; ++i) {
         std::string v;
         if (flag(argc, argv, i, "photon_n", v)) photon_n = std::atoll(v.c_str());
@@ -68,6 +69,7 @@ int main(int argc, char **argv) {
         else if (flag(argc, argv, i, "seed", v)) seed = std::strtoull(v.c_str(), nullptr, 10);
         else if (flag(argc, argv, i, "batch", v)) batch = std::atoll(v.c_str());
         else if (flag(argc, argv, i, "threads", v)) threads = std::atoi(v.c_str());
+        else if (std::strcmp(argv[i], "--host_emit") == 0) host_emit = true;
         else {
             std::fprintf(stderr, "unknown argument %s\n", argv[i]);
             return 2;
@@ -99,7 +101,13 @@ int main(int argc, char **argv) {
     }
     grm_engine_set_option(e, GRM_OPT_SEED, (int64_t)seed);
 
-    /* run_simulation: zone-range batches so emission of the next batch overlaps transport */
+    /* run_simulation: zone-range batches (bounded HBM for the emitted photons), each emitted on the
+     * GPU from the zone table and tracked there; --host_emit keeps the host emitter (batch b+1
+     * emitted on host threads while batch b is tracked) */
+    if (!host_emit && grm_engine_emit_setup_from_model(e, m)) {
+        std::fprintf(stderr, "[error] emission setup: %s %s\n", grm_engine_last_error(e), grm_model_last_error());
+        return 1;
+    }
     info("Starting main loop");
     const auto t0 = std::chrono::steady_clock::now();
     grm_header h;
@@ -125,19 +133,30 @@ int main(int argc, char **argv) {
         buf.resize((size_t)std::max<int64_t>(n, 0));
         if (n > 0) grm_model_emit(m, seed, cuts[b], cuts[b + 1], buf.data(), buf.size(), threads);
     };
-    emit(0, cur);
+    if (host_emit) emit(0, cur);
     for (size_t b = 0; b + 1 < cuts.size(); ++b) {
-        std::thread prod;
-        if (b + 2 < cuts.size()) prod = std::thread(emit, b + 1, std::ref(nxt));
-        if (!cur.empty() && grm_engine_track(e, cur.data(), cur.size())) {
-            std::fprintf(stderr, "[error] transport: %s\n", grm_engine_last_error(e));
+        if (host_emit) {
+            std::thread prod;
+            if (b + 2 < cuts.size()) prod = std::thread(emit, b + 1, std::ref(nxt));
+            if (!cur.empty() && grm_engine_track(e, cur.data(), cur.size())) {
+                std::fprintf(stderr, "[error] transport: %s\n", grm_engine_last_error(e));
+                if (prod.joinable()) prod.join();
+                return 1;
+            }
+            created += cur.size();
             if (prod.joinable()) prod.join();
-            return 1;
+            std::swap(cur, nxt);
+            nxt.clear();
+        } else {
+            grm_init_photon *d_ph = nullptr;
+            uint64_t n = 0;
+            if (grm_engine_emit(e, seed, cuts[b], cuts[b + 1], &d_ph, &n) ||
+                (n && grm_engine_track_device(e, d_ph, n))) {
+                std::fprintf(stderr, "[error] emission/transport: %s\n", grm_engine_last_error(e));
+                return 1;
+            }
+            created += n;
         }
-        created += cur.size();
-        if (prod.joinable()) prod.join();
-        std::swap(cur, nxt);
-        nxt.clear();
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         info("Rate %.2f ph/s, zone batch %zu/%zu", created / el, b + 1, cuts.size() - 1);
     }
