@@ -37,6 +37,37 @@ constexpr double JNU_MAX_T = 1.0e2, JNU_CST = 1.88774862536;
 constexpr double SPEC_D_L_E = 0.25;
 constexpr int N_TH_BINS = GRM_N_TH_BINS, N_E_BINS = GRM_N_E_BINS;
 
+/* ---- division ----
+ * An IEEE fp64 divide is 11 VALU ops on CDNA (div_scale x2, rcp, 5 fma, mul, div_fmas, div_fixup).
+ * The transport step's divisors are finite, normal, non-zero physical quantities, so the hot path
+ * divides with v_rcp_f64 + two Newton steps + one residual correction (7 ops, <= 1 ulp from the
+ * correctly rounded quotient -- below the fp-contraction differences the CPU reference already has
+ * from one compiler to another).  -DGRM_EXACT_DIV restores plain '/' (A/B builds). */
+#ifndef GRM_EXACT_DIV
+__device__ __forceinline__ double frcp(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-b, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ __forceinline__ double fdiv(double a, double b) {
+    const double r = frcp(b);
+    const double q = a * r;
+    return fma(fma(-b, q, a), r, q);
+}
+/* |a| / |b| for a tolerance test only (one Newton step, ~1e-16 relative) */
+__device__ __forceinline__ double fratio_tol(double a, double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(r, fma(-b, r, 1.0), r);
+    return fabs(a * r);
+}
+#else
+__device__ __forceinline__ double frcp(double b) { return 1.0 / b; }
+__device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
+__device__ __forceinline__ double fratio_tol(double a, double b) { return fabs(a / b); }
+#endif
+
 /* Kernel-argument block: everything uniform across lanes (lands in SGPRs). */
 struct Params {
     int n1, n2;
@@ -147,15 +178,15 @@ __device__ __forceinline__ void gcov_from_trig(const Params &P, const Trig &T, G
     const double rho2 = r * r + a * a * cos_theta * cos_theta;
     const double rfac = r - P.r0;
     const double hfac = kPi + (1.0 - P.h_slope) * kPi * T.c2x;
-    const double two_r_rho2 = 2.0 * r / rho2;
+    const double irho2 = frcp(rho2);
+    const double two_r_rho2 = 2.0 * r * irho2;
     G.g00 = (-1.0 + two_r_rho2);
     G.g01 = two_r_rho2 * rfac;
-    G.g03 = (-2.0 * a * r * s2 / rho2);
+    G.g03 = -2.0 * a * r * s2 * irho2;
     G.g11 = (1.0 + two_r_rho2) * rfac * rfac;
     G.g13 = (-a * s2 * (1.0 + two_r_rho2)) * rfac;
     G.g22 = rho2 * hfac * hfac;
     G.g33 = s2 * (rho2 + a * a * s2 * (1.0 + two_r_rho2));
-    const double irho2 = 1.0 / rho2;
     G.gn00 = -1.0 - 2.0 * r * irho2;
     G.gn01 = 2.0 * irho2;
 }
@@ -195,13 +226,13 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
     const double a = P.a, a2 = a * a, a3 = a2 * a, a4 = a3 * a;
     const double a2sth2 = a2 * sth2, a2cth2 = a2 * cth2, a4cth4 = a4 * cth4;
     const double rho2 = r2 + a2cth2, rho22 = rho2 * rho2, rho23 = rho22 * rho2;
-    const double irho2 = 1.0 / rho2, irho22 = irho2 * irho2, irho23 = irho22 * irho2;
-    const double irho23_dthdx2 = irho23 / dthdx2;
+    const double irho2 = frcp(rho2), irho22 = irho2 * irho2, irho23 = irho22 * irho2;
+    const double idthdx2 = frcp(dthdx2), irho23_dthdx2 = irho23 * idthdx2;
     const double fac1 = r2 - a2cth2, fac1_rho23 = fac1 * irho23;
     const double fac2 = a2 + 2.0 * r2 + a2 * c2th;
     const double fac3 = a2 + r1 * (-2.0 + r1);
-    const double i_r1rho23 = 1.0 / (r1 * rho23);
-    const double i_sth = 1.0 / sth;
+    const double i_r1rho23 = frcp(r1) * irho23;
+    const double i_sth = frcp(sth), ifac2 = frcp(fac2);
 
     C.c[0][0] = 2.0 * r1 * fac1_rho23;
     C.c[0][1] = r1 * (2.0 * r1 + rho2) * fac1_rho23;
@@ -222,7 +253,7 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
                  a2 * (a2 * r1 * (1.0 + 3.0 * r1) * cth4 + a4cth4 * cth2 + r3 * sth2 +
                        r1 * cth2 * (2.0 * r1 + 3.0 * r3 - a2sth2))) *
                 irho23;
-    C.c[1][5] = -a2 * dthdx2 * s2th / fac2;
+    C.c[1][5] = -a2 * dthdx2 * s2th * ifac2;
     C.c[1][6] = a * sth2 * (a4 * r1 * cth4 + r2 * (2.0 * r1 + r3 - a2sth2) + a2cth2 * (2.0 * r1 * (-1.0 + r2) + a2sth2)) *
                 irho23;
     C.c[1][7] = -fac3 * dthdx22 * irho2;
@@ -237,17 +268,17 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
     C.c[2][5] = r2 * irho2;
     C.c[2][6] = (a * r1 * cth * sth * (r3 * (2.0 + r1) + a2 * (2.0 * r1 * (1.0 + r1) * cth2 + a2 * cth4 + 2.0 * r1sth2))) *
                 irho23_dthdx2;
-    C.c[2][7] = -a2 * cth * sth * dthdx2 * irho2 + d2thdx22 / dthdx2;
+    C.c[2][7] = -a2 * cth * sth * dthdx2 * irho2 + d2thdx22 * idthdx2;
     C.c[2][8] = 0.0;
     C.c[2][9] = -cth * sth * (rho23 + a2sth2 * rho2 * (r1 * (4.0 + r1) + a2cth2) + 2.0 * r1 * a4 * sth4) *
                 irho23_dthdx2;
 
     C.c[3][0] = a * fac1_rho23;
     C.c[3][1] = r1 * C.c[3][0];
-    C.c[3][2] = -2.0 * a * r1 * cth * dthdx2 * i_sth / rho22;
+    C.c[3][2] = -2.0 * a * r1 * cth * dthdx2 * i_sth * irho22;
     C.c[3][3] = -a2sth2 * fac1_rho23;
     C.c[3][4] = a * r2 * fac1_rho23;
-    C.c[3][5] = -2 * a * r1 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * cth * dthdx2 * i_sth / (fac2 * fac2);
+    C.c[3][5] = -2 * a * r1 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * cth * dthdx2 * i_sth * (ifac2 * ifac2);
     C.c[3][6] = r1 * (r1 * rho22 - a2sth2 * fac1) * irho23;
     C.c[3][7] = -a * r1 * dthdx22 * irho2;
     C.c[3][8] = dthdx2 * (0.25 * fac2 * fac2 * cth * i_sth + a2 * r1 * s2th) * irho22;
@@ -274,13 +305,13 @@ __device__ __forceinline__ void init_dkdlam(const Params &P, const double x[4], 
 
 /* harm_model.cpp:1620-1630 */
 __device__ __forceinline__ double step_size(const Params &P, const double x[4], const double k[4]) {
-    const double dl_x_1 = STEP_EPS * x[1] / (fabs(k[1]) + EPS);
-    const double dl_x_2 = STEP_EPS * fmin(x[2], P.xe2 - x[2]) / (fabs(k[2]) + EPS);
-    const double dl_x_3 = STEP_EPS / (fabs(k[3]) + EPS);
-    const double i1 = 1.0 / (fabs(dl_x_1) + EPS);
-    const double i2 = 1.0 / (fabs(dl_x_2) + EPS);
-    const double i3 = 1.0 / (fabs(dl_x_3) + EPS);
-    return 1.0 / (i1 + i2 + i3);
+    const double dl_x_1 = fdiv(STEP_EPS * x[1], fabs(k[1]) + EPS);
+    const double dl_x_2 = fdiv(STEP_EPS * fmin(x[2], P.xe2 - x[2]), fabs(k[2]) + EPS);
+    const double dl_x_3 = fdiv(STEP_EPS, fabs(k[3]) + EPS);
+    const double i1 = frcp(fabs(dl_x_1) + EPS);
+    const double i2 = frcp(fabs(dl_x_2) + EPS);
+    const double i3 = frcp(fabs(dl_x_3) + EPS);
+    return frcp(i1 + i2 + i3);
 }
 
 /* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
@@ -317,15 +348,17 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
         for (int i = 0; i < 4; ++i) {
             dk[i] = geo_rhs(C, i, kc);
             kp[i] = k[i] + dl_2 * dk[i];
-            err += fabs((kc[i] - kp[i]) / (kp[i] + EPS));
+            err += fratio_tol(kc[i] - kp[i], kp[i] + EPS);
         }
     } while (err > E_TOL && iter < MAX_ITER);
 #pragma unroll
     for (int i = 0; i < 4; ++i) k[i] = kp[i];
     gcov_from_trig(P, T, G);
     e_1 = -(k[0] * G.g00 + k[1] * G.g01 + k[3] * G.g03);
-    const double err_e = fabs((e_1 - e_0_s) / e_0_s);
-    return (err_e > 1.0e-4 || err > E_TOL || isnan(err) || isinf(err));
+    /* |(e_1 - e_0_s) / e_0_s| > 1e-4 without the divide: same outcome for e_0_s = 0 (0/0 = NaN
+     * fails neither test, x/0 = inf passes both) and NaN operands */
+    const bool err_e = fabs(e_1 - e_0_s) > 1.0e-4 * fabs(e_0_s);
+    return (err_e || err > E_TOL || isnan(err) || isinf(err));
 }
 
 /* Per-lane spill slot for the push backup, laid out [component][lane] so that a wave's
@@ -388,8 +421,9 @@ struct Fluid {
  * edge clamp of interp_scalar); false = out of the grid */
 __device__ __forceinline__ bool zone_index(const Params &P, const double x[4], int &i, int &j, double &di, double &dj) {
     if (x[1] < P.xs1 || x[1] > P.xe1 || x[2] < P.xs2 || x[2] > P.xe2) return false;
-    i = (int)((x[1] - P.xs1) / P.dx1 - 0.5 + 1000) - 1000;
-    j = (int)((x[2] - P.xs2) / P.dx2 - 0.5 + 1000) - 1000;
+    const double t1 = fdiv(x[1] - P.xs1, P.dx1), t2 = fdiv(x[2] - P.xs2, P.dx2);
+    i = (int)(t1 - 0.5 + 1000) - 1000;
+    j = (int)(t2 - 0.5 + 1000) - 1000;
     if (i < 0) {
         i = 0;
         di = 0.0;
@@ -397,7 +431,7 @@ __device__ __forceinline__ bool zone_index(const Params &P, const double x[4], i
         i = P.n1 - 2;
         di = 1.0;
     } else {
-        di = (x[1] - ((i + 0.5) * P.dx1 + P.xs1)) / P.dx1;
+        di = t1 - (i + 0.5);
     }
     if (j < 0) {
         j = 0;
@@ -406,7 +440,7 @@ __device__ __forceinline__ bool zone_index(const Params &P, const double x[4], i
         j = P.n2 - 2;
         dj = 1.0;
     } else {
-        dj = (x[2] - ((j + 0.5) * P.dx2 + P.xs2)) / P.dx2;
+        dj = t2 - (j + 0.5);
     }
     return true;
 }
@@ -452,18 +486,18 @@ __device__ __forceinline__ void fluid_from(const Params &P, const double x[4], c
     }
     const double rho = v[0], uu = v[1];
     F.n_e = rho * P.n_e_unit;
-    F.theta_e = uu / rho * P.theta_e_unit;
+    F.theta_e = fdiv(uu, rho) * P.theta_e_unit;
     const double vc1 = v[2], vc2 = v[3], vc3 = v[4];
     const double bp1 = v[5], bp2 = v[6], bp3 = v[7];
     const double vdv = G.g11 * vc1 * vc1 + G.g13 * vc1 * vc3 + G.g22 * vc2 * vc2 + G.g13 * vc3 * vc1 + G.g33 * vc3 * vc3;
-    const double vfac = sqrt(-1.0 / G.gn00 * (1.0 + fabs(vdv)));
+    const double vfac = sqrt(-frcp(G.gn00) * (1.0 + fabs(vdv)));
     F.u_con[0] = -vfac * G.gn00;
     F.u_con[1] = vc1 - vfac * G.gn01;
     F.u_con[2] = vc2;
     F.u_con[3] = vc3;
     lower(G, F.u_con, F.u_cov);
     const double udb = F.u_cov[1] * bp1 + F.u_cov[2] * bp2 + F.u_cov[3] * bp3;
-    const double iu0 = 1.0 / F.u_con[0];
+    const double iu0 = frcp(F.u_con[0]);
     F.b_con[0] = udb;
     F.b_con[1] = (bp1 + F.u_con[1] * udb) * iu0;
     F.b_con[2] = (bp2 + F.u_con[2] * udb) * iu0;
@@ -496,14 +530,14 @@ __device__ __forceinline__ double bk_angle(const double k[4], const Fluid &F, do
 __device__ __forceinline__ double bk_sin(const double k[4], const Fluid &F, double b_unit) {
     if (F.b == 0.0) return 1.0;
     const double k_ = fabs(k[0] * F.u_cov[0] + k[1] * F.u_cov[1] + k[2] * F.u_cov[2] + k[3] * F.u_cov[3]);
-    double mu = (k[0] * F.b_cov[0] + k[1] * F.b_cov[1] + k[2] * F.b_cov[2] + k[3] * F.b_cov[3]) / (k_ * F.b / b_unit);
+    double mu = fdiv((k[0] * F.b_cov[0] + k[1] * F.b_cov[1] + k[2] * F.b_cov[2] + k[3] * F.b_cov[3]) * b_unit, k_ * F.b);
     mu = fmin(fmax(mu, -1.0), 1.0);
     return sqrt((1.0 - mu) * (1.0 + mu));
 }
 
 __device__ __forceinline__ double fluid_nu(const double k[4], const Fluid &F) {
     const double energy = -(k[0] * F.u_cov[0] + k[1] * F.u_cov[1] + k[2] * F.u_cov[2] + k[3] * F.u_cov[3]);
-    return energy * ME * CL * CL / HPL;
+    return energy * (ME * CL * CL / HPL);
 }
 
 __device__ __forceinline__ double hc_klein_nishina(double w) { /* hotcross.cpp:144-151 */
@@ -623,6 +657,82 @@ __device__ __forceinline__ double alpha_inv_abs_s(const Params &P, double nu, do
 __device__ __forceinline__ double alpha_inv_abs(const Params &P, double nu, double theta_e, double n_e, double b,
                                                 double theta) {
     return alpha_inv_abs_s(P, nu, theta_e, n_e, b, sin(theta), log(theta_e));
+}
+
+/* alpha_inv_scatt + alpha_inv_abs together (radiation.cpp:103-146, hotcross.cpp:81-106,
+ * jnu_mixed.cpp:75-111), the formulas of the separate functions above (constant factors folded,
+ * divisions through fdiv: agreement to a few ulp, tests/test_gpu_probes.py), scheduled for one wave per
+ * SIMD: both table indices are formed first and all six table loads (hotcross 4, K2 2) are issued
+ * unconditionally (index 0 when a branch does not use the table), so their L2 latency overlaps
+ * sin(theta), the synchrotron and Planck terms instead of being exposed twice in a row. */
+__device__ __forceinline__ void radiation_coeffs(const Params &P, const double k[4], const Fluid &F, double nu,
+                                                 double &a_s, double &a_a) {
+    const double theta_e = F.theta_e, n_e = F.n_e, b = F.b;
+    const double ln_te = log(theta_e);
+    /* hotcross lookup index (hotcross.cpp:82-100) */
+    const double w = nu * (HPL / (ME * CL * CL));
+    const bool hc_thomson = w * theta_e < 1.0e-6;
+    const bool hc_kn = !hc_thomson && theta_e < HC_MIN_T;
+    const bool hc_num =
+        !hc_thomson && !hc_kn && (w <= HC_MIN_W || w >= HC_MAX_W || theta_e <= HC_MIN_T || theta_e >= HC_MAX_T);
+    const bool hc_table = !hc_thomson && !hc_kn && !hc_num;
+    double fi = 0.0, fj = 0.0;
+    if (hc_table) {
+        fi = fdiv(log10(w) - P.hc_l_min_w, P.hc_d_l_w);
+        fj = fdiv(ln_te * kLog10E - P.hc_l_min_t, P.hc_d_l_t);
+    }
+    const int i = hc_table ? (int)fi : 0, j = hc_table ? (int)fj : 0;
+    /* K2 index (jnu_mixed.cpp:102-111, 150-158) */
+    const bool k2_table = !(theta_e < THETA_E_MIN) && !(theta_e > JNU_MAX_T);
+    double dk = k2_table ? fdiv(ln_te - P.jnu_l_min_t, P.jnu_d_l_t) : 0.0;
+    const int ik = k2_table ? min((int)dk, GRM_N_E_SAMP - 1) : 0;
+    const double *t = P.hotcross + (size_t)i * (HC_N_T + 1) + j;
+    const double t00 = t[0], t01 = t[1], t10 = t[HC_N_T + 1], t11 = t[HC_N_T + 2];
+    const double k2a = P.k2[ik], k2b = P.k2[ik + 1];
+    /* table-independent work while the loads are in flight: sin(theta) (bk_sin), the synchrotron
+     * frequency terms, the Planck denominator */
+    const double sin_theta = bk_sin(k, F, P.b_unit);
+    const double nu_c = b * (EE / (2.0 * kPi * ME * CL));
+    const double nu_s = (2.0 / 9.0) * nu_c * theta_e * theta_e * sin_theta;
+    const double x = fdiv(nu, nu_s);
+    const double xp = cbrt(x);
+    const double xx = sqrt(x) + JNU_CST * sqrt(xp);
+    const double f = xx * xx;
+    const double ex = exp(-xp);
+    const double xb = fdiv(w, theta_e);
+    double b_nu;
+    if (xb < 1.0e-3)
+        b_nu = fdiv(2.0 * HPL / (CL * CL), xb * (1.0 / 24.0) * (24.0 + xb * (12.0 + xb * (4.0 + xb))));
+    else
+        b_nu = fdiv(2.0 * HPL / (CL * CL), exp(xb) - 1.0);
+    /* scattering: kappa_es * nu * n_e * m_p */
+    double sigma;
+    if (hc_thomson) {
+        sigma = SIGMA_THOMSON;
+    } else if (hc_kn) {
+        sigma = hc_klein_nishina(w) * SIGMA_THOMSON;
+    } else if (hc_num) {
+        sigma = hotcross_num(w, theta_e);
+    } else {
+        const double d_i = fi - i, d_j = fj - j;
+        const double lc =
+            (1.0 - d_i) * (1.0 - d_j) * t00 + d_i * (1.0 - d_j) * t10 + (1.0 - d_i) * d_j * t01 + d_i * d_j * t11;
+        sigma = exp10(lc);
+    }
+    a_s = nu * sigma * n_e; /* nu kappa n_e m_p, kappa = sigma / m_p */
+    /* absorption: j_nu / nu^2 / (B_nu / nu^3) */
+    double jnu = 0.0;
+    if (!(theta_e < THETA_E_MIN) && !(nu > 1.0e12 * nu_s)) {
+        double k2;
+        if (theta_e > JNU_MAX_T) {
+            k2 = 2.0 * theta_e * theta_e;
+        } else {
+            dk -= ik;
+            k2 = exp((1.0 - dk) * k2a + dk * k2b);
+        }
+        jnu = fdiv((kSqrt2 * kPi * EE * EE / (3.0 * CL)) * n_e * nu_s, k2) * f * ex;
+    }
+    a_a = fdiv(jnu, nu * nu * (b_nu + 1.0e-100));
 }
 
 /* ------------------------------------------------------------------------- */

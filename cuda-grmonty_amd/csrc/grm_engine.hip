@@ -78,7 +78,7 @@ static_assert(sizeof(Cold) == 80, "Cold layout");
 struct DevCounters {
     unsigned long long n_recorded, n_scatt, max_tau_bits, n_steps;
     unsigned long long n_tracked, n_children, n_overflow, n_dropped;
-    unsigned long long n_primaries, max_nstep, n_long, pad[5];
+    unsigned long long n_primaries, max_nstep, n_long, n_abandoned, abort, n_nan, pad[2];
 };
 
 struct Ctl {
@@ -111,7 +111,14 @@ struct Ctl {
     unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     int lanes;
+    /* watchdog: a launch older than watchdog_ticks (s_memrealtime, 100 MHz; 0 = off) abandons its
+     * photons and exits, so no input can keep the GPU busy without bound.  The first stuck_cap
+     * abandoned lanes leave a STUCK_WORDS-double record (grm_engine_debug_stuck). */
+    unsigned long long watchdog_ticks;
+    double *stuck;
+    unsigned long long stuck_cap, *stuck_count;
 };
+constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 
 /* hot photon state: lives in VGPRs for the photon's whole life */
 struct Lane {
@@ -158,7 +165,7 @@ __device__ __forceinline__ double bias_den(const Params &P, const Ctl &C) {
 /* bias_func (harm_model.cpp:1391-1404), same expression and rounding as the reference */
 __device__ __forceinline__ double bias_func(double den, double t_e, double w) {
     const double max = 0.5 * w / WEIGHT_MIN;
-    double bias = 100.0 * t_e * t_e / den;
+    double bias = fdiv(100.0 * t_e * t_e, den);
     if (bias < TP_OVER_TE) bias = TP_OVER_TE;
     if (bias > max) bias = max;
     return bias / TP_OVER_TE;
@@ -333,9 +340,7 @@ __device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lan
     Fluid F;
     fluid_params(P, L.x, G, F);
     const double nu = fluid_nu(L.k, F);
-    const double ln_te = log(F.theta_e);
-    L.alpha_scatti = alpha_inv_scatt(P, nu, F.theta_e, F.n_e, ln_te);
-    L.alpha_absi = alpha_inv_abs_s(P, nu, F.theta_e, F.n_e, F.b, bk_sin(L.k, F, P.b_unit), ln_te);
+    radiation_coeffs(P, L.k, F, nu, L.alpha_scatti, L.alpha_absi);
     L.bi = bias_func(bias_d, F.theta_e, L.w);
     L.fl_ne = F.n_e;
     Conn Cn;
@@ -602,6 +607,16 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             end_of_life(P, C, cold, L);
             return false;
         }
+        /* A NaN position is absorbing: every later stop test is false, no interaction can fire
+         * (bias * d_tau_scatt > x1 is false for NaN), and record_super_photon drops NaN photons
+         * (harm_model.cpp:1291-1295), so the reference's loop only burns steps -- each a full
+         * 255-attempt halving tree, since err is NaN -- until max_n_step (:1058-1063, no record :1066).  End it here
+         * with the same (empty) outcome. */
+        if (isnan(L.x[1])) {
+            atomicAdd(&C.ctr->n_nan, 1ull);
+            trace_end(C, cold, L, 3);
+            return false;
+        }
     }
     TSTAMP(10);
     if (at_scatter || L.alpha_absi > 0.0 || L.alpha_scatti > 0.0 || L.fl_ne > 0.0) {
@@ -628,10 +643,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         const bool zero = nu < 0.0 || (!at_scatter && F.n_e == 0.0);
         double a_s = 0.0, a_a = 0.0;
         if (!zero) {
-            const double sth = bk_sin(L.k, F, P.b_unit);
-            const double ln_te = log(F.theta_e);
-            a_s = alpha_inv_scatt(P, nu, F.theta_e, F.n_e, ln_te);
-            a_a = alpha_inv_abs_s(P, nu, F.theta_e, F.n_e, F.b, sth, ln_te);
+            radiation_coeffs(P, L.k, F, nu, a_s, a_a);
         }
         const double bf = (zero && !at_scatter) ? 0.0 : bias_func(bias_d, F.theta_e, L.w);
         TSTAMP(12);
@@ -664,9 +676,9 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             L.alpha_absi = a_a;
             L.bi = bf;
             const double x1 = -log(uniform(L.rng));
-            const double wc = L.w / bias;
+            const double wc = fdiv(L.w, bias);
             if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) {
-                const double frac = x1 / (bias * d_tau_scatt);
+                const double frac = fdiv(x1, bias * d_tau_scatt);
                 d_tau_abs *= frac;
                 if (d_tau_abs > 100) {
                     trace_end(C, cold, L, 2);
@@ -713,6 +725,25 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     return true;
 }
 
+/* watchdog record of a photon abandoned mid-flight: id, n_step, phase, depth, pend, w, e_0_s, dl, x, k */
+__device__ void record_stuck(const Ctl &C, const Lane &L) {
+    const unsigned long long slot = atomicAdd(C.stuck_count, 1ull);
+    if (slot >= C.stuck_cap) return;
+    double *r = C.stuck + slot * STUCK_WORDS;
+    r[0] = (double)L.rng.id;
+    r[1] = L.n_step;
+    r[2] = L.phase;
+    r[3] = L.depth;
+    r[4] = L.pend;
+    r[5] = L.w;
+    r[6] = L.e_0_s;
+    r[7] = L.dl;
+    for (int i = 0; i < 4; ++i) {
+        r[8 + i] = L.x[i];
+        r[12 + i] = L.k[i];
+    }
+}
+
 __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P, Ctl C) {
 #ifdef GRM_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
@@ -754,6 +785,23 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         if ((trip++ & 15) == 0 || warm) {
             flush_counters(C);
             if (!C.bias_frozen) bias_d = bias_den(P, C);
+            if (C.watchdog_ticks) {
+                bool stop = __hip_atomic_load(&C.ctr->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (!stop && __builtin_amdgcn_s_memrealtime() - rt_start > C.watchdog_ticks) {
+                    stop = true;
+                    if (lane_id == 0) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (stop) { /* abandon: drop the lane photons, the wave's stack and the pool; exit */
+                    if (active) {
+                        record_stuck(C, L);
+                        atomicAdd(&C.ctr->n_abandoned, 1ull);
+                        active = false;
+                    }
+                    pool_done = true;
+                    warm = false;
+                    if (lane_id == 0) *wtop = 0;
+                }
+            }
             TSTAMP(7);
         }
         /* Batched refill (converged point).  Idle lanes wait until at least refill_min of them can
@@ -976,6 +1024,8 @@ struct grm_engine {
     ncclComm_t comm = nullptr;
     unsigned long long *d_timing = nullptr;
     unsigned long long *d_waves = nullptr; /* [lanes / 64][4] per-wave record of the last launch */
+    int64_t watchdog_ms = 60000;           /* per-launch watchdog (GRM_OPT_WATCHDOG_MS; 0 = off) */
+    double *d_stuck = nullptr;             /* [STUCK_CAP][STUCK_WORDS] abandoned-photon records */
     /* device emission: zone table, emission tables, zone offsets, emitted photons */
     grm_emit_zone *d_ezones = nullptr;
     double *d_eweight = nullptr, *d_ef = nullptr;
@@ -1062,6 +1112,10 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     C.bias_frozen = e->bias_mode;
     C.in_flight = e->d_small + 4;
     C.admit_end = e->d_small + 5;
+    C.watchdog_ticks = (unsigned long long)std::max<int64_t>(e->watchdog_ms, 0) * 100000ull; /* 100 MHz */
+    C.stuck = e->d_stuck;
+    C.stuck_cap = STUCK_CAP;
+    C.stuck_count = e->d_small + 6;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
@@ -1112,6 +1166,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
             C.n_pool = n_pool;
             C.admit_n = 0;
         }
+        HIPCHK(e, hipMemsetAsync(&e->d_ctr->abort, 0, sizeof(unsigned long long), e->stream));
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
         hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
         HIPCHK(e, hipGetLastError());
@@ -1130,6 +1185,14 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
         }
         steps_pass = hp.n_steps;
         e->stats.n_launches++;
+        e->stats.n_nan_photons = hp.n_nan;
+        if (hp.abort) {
+            e->stats.n_abandoned = hp.n_abandoned;
+            e->err = "watchdog: a transport launch ran longer than " + std::to_string(e->watchdog_ms) + " ms; " +
+                     std::to_string(hp.n_abandoned) +
+                     " photons abandoned (their state: grm_engine_debug_stuck); results of this call are incomplete";
+            return -1;
+        }
         n_pool = std::min(cnt, e->ovf_cap);
         src = dst;
         dst ^= 1;
@@ -1177,6 +1240,7 @@ int reset_counters(grm_engine *e) {
     std::memcpy(&h.max_tau_bits, &e->max_tau_init, sizeof(double));
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_small, 0, 4 * sizeof(unsigned long long), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_small + 6, 0, sizeof(unsigned long long), e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return 0;
 }
@@ -1213,7 +1277,9 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
         !hip_ok(e, hipMalloc(&e->d_k2, (GRM_N_E_SAMP + 1) * sizeof(double)), "k2") ||
         !hip_ok(e, hipMalloc(&e->d_ctr, sizeof(DevCounters)), "counters") ||
         !hip_ok(e, hipMalloc(&e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS), "spectrum") ||
-        !hip_ok(e, hipMalloc(&e->d_small, 8 * sizeof(unsigned long long)), "small"))
+        !hip_ok(e, hipMalloc(&e->d_small, 8 * sizeof(unsigned long long)), "small") ||
+        !hip_ok(e, hipMalloc(&e->d_stuck, STUCK_CAP * STUCK_WORDS * sizeof(double)), "stuck") ||
+        !hip_ok(e, hipMemset(e->d_small, 0, 8 * sizeof(unsigned long long)), "small"))
         return fail();
     if (!hip_ok(e, hipMemcpy(e->d_zones, zones.data(), nz * 8 * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
         !hip_ok(e, hipMemcpy(e->d_hot, hotcross, nhot * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
@@ -1273,6 +1339,7 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_ovf[0]);
     hipFree(e->d_ovf[1]);
     hipFree(e->d_small);
+    hipFree(e->d_stuck);
     hipFree(e->d_batch);
     hipFree(e->d_trace);
     hipFree(e->d_upload);
@@ -1314,6 +1381,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_FROZEN_MAXTAU: std::memcpy(&e->fz_maxtau, &v, sizeof(double)); e->frozen_set = true; return 0;
     case GRM_OPT_WARMUP: e->warmup = v; return 0;
     case GRM_OPT_REFILL_MIN: e->refill_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
+    case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }
 }
@@ -1500,6 +1568,17 @@ int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap) {
     const size_t n = e->lanes / 64;
     const size_t k = std::min(n, cap);
     if (k && out && hipMemcpy(out, e->d_waves, k * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return (int64_t)n;
+}
+
+int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap) {
+    if (!e || !e->d_small) return -1;
+    if (hipSetDevice(e->device) != hipSuccess) return -1;
+    unsigned long long cnt = 0;
+    if (hipMemcpy(&cnt, e->d_small + 6, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    const size_t n = std::min<size_t>(cnt, STUCK_CAP), k = std::min(n, cap);
+    if (k && out && hipMemcpy(out, e->d_stuck, k * STUCK_WORDS * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return (int64_t)n;
 }

@@ -9,7 +9,7 @@
  *  2     x[4]                                       Gamma[4][4][4] (j<=k filled, rest 0)
  *  3     x[4] k[4] dk[4] e_0_s dl                   x[4] k[4] dk[4] e_0_s   (push_photon)
  *  4     x[4]                                       n_e theta_e b u_con u_cov b_con b_cov (19)
- *  5     x[4] k[4]                                  theta nu alpha_scatt alpha_abs
+ *  5     x[4] k[4]                                  theta nu alpha_scatt alpha_abs (fused), same (separate)
  *  6     w theta_e                                  sigma_hot (lookup)
  *  7     nu n_e theta_e b theta                     j_nu (synch)
  *  8     theta_e                                    K2 (k2_eval)
@@ -117,8 +117,12 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
             const double nu = fluid_nu(k, F);
             store(o, 0, th);
             store(o, 1, nu);
-            store(o, 2, alpha_inv_scatt(P, nu, F.theta_e, F.n_e));
-            store(o, 3, alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, th));
+            double a_s, a_a; /* the transport kernel's fused evaluation */
+            radiation_coeffs(P, k, F, nu, a_s, a_a);
+            store(o, 2, a_s);
+            store(o, 3, a_a);
+            store(o, 4, alpha_inv_scatt(P, nu, F.theta_e, F.n_e)); /* the separate functions */
+            store(o, 5, alpha_inv_abs(P, nu, F.theta_e, F.n_e, F.b, th));
         }
         break;
     }

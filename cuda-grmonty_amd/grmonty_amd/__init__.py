@@ -45,6 +45,7 @@ EMIT_ZONE = np.dtype([("nz", "<f8"), ("dn_max", "<f8"), ("x", "<f8", 4), ("n_e",
 
 OPT_SEED, OPT_BIAS_MODE, OPT_TRACE_CAP, OPT_GRID_BLOCKS, OPT_ID_BASE = 0, 1, 2, 3, 4
 OPT_FROZEN_SCATT, OPT_FROZEN_REC, OPT_FROZEN_MAXTAU, OPT_WARMUP, OPT_REFILL_MIN = 5, 6, 7, 8, 9
+OPT_WATCHDOG_MS = 10
 N_TH_BINS, N_E_BINS = 6, 200
 
 
@@ -68,7 +69,8 @@ class Stats(C.Structure):
                 ("n_launches", C.c_uint64), ("kernel_ms", C.c_double), ("last_kernel_ms", C.c_double),
                 ("last_steps", C.c_uint64), ("last_emit_ms", C.c_double),
                 ("max_launch_ms", C.c_double), ("max_launch_steps", C.c_uint64),
-                ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64)]
+                ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64), ("n_abandoned", C.c_uint64),
+                ("n_nan_photons", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -113,6 +115,7 @@ SIGNATURES = {
     "grm_engine_allreduce": (C.c_int, [VP]),
     "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
     "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
+    "grm_engine_debug_stuck": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_sizeof": (C.c_size_t, [C.c_int]),
     "grm_version": (C.c_char_p, []),
 }
@@ -348,6 +351,14 @@ class Engine:
         out = np.zeros((n, 4), dtype=np.uint64)
         self.L.grm_engine_debug_waves(self.h, _ptr(out), n)
         return out
+
+    def debug_stuck(self) -> np.ndarray:
+        """Photons the launch watchdog abandoned: id, n_step, phase, depth, pend, w, e_0_s, dl, x[4], k[4]."""
+        out = np.zeros((256, 16), dtype=np.float64)
+        n = self.L.grm_engine_debug_stuck(self.h, _ptr(out), 256)
+        if n < 0:
+            raise RuntimeError(self.error())
+        return out[:n]
 
     def allreduce(self):
         self._check(self.L.grm_engine_allreduce(self.h))

@@ -115,6 +115,8 @@ typedef struct grm_stats {
     uint64_t max_launch_steps; /* ... and the transport steps it made (per-launch roofline) */
     uint64_t max_photon_steps; /* longest superphoton life (n_step) since the last reset */
     uint64_t n_long_photons;   /* superphotons that lived more than 100k steps since the last reset */
+    uint64_t n_abandoned;      /* photons dropped by the launch watchdog (GRM_OPT_WATCHDOG_MS); 0 in a good run */
+    uint64_t n_nan_photons;    /* superphotons ended at a NaN position since the last reset (see grm_engine.hip) */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
@@ -136,7 +138,12 @@ enum {
     GRM_OPT_WARMUP = 8,
     /* idle lanes a wavefront gathers before it refills them together (1..64, default 16):
      * larger = less divergent child sampling / photon set-up, more idle lane-trips */
-    GRM_OPT_REFILL_MIN = 9
+    GRM_OPT_REFILL_MIN = 9,
+    /* per-launch watchdog in ms (default 60000, 0 = off): a transport launch running longer abandons
+     * its photons and exits, and the track call fails with the reason in grm_engine_error -- no input
+     * can keep the GPU busy without bound (a photon's life is bounded only by 1.28M steps x 255
+     * halving attempts) */
+    GRM_OPT_WATCHDOG_MS = 10
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
@@ -178,6 +185,10 @@ int grm_engine_debug_timing(grm_engine *e, uint64_t out[16], int reset);
  * (s_memrealtime, 100 MHz), loop trips, superphotons tracked.  out holds cap waves; returns the
  * number of waves of the grid (-1 before the first launch). */
 int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap);
+
+/* diagnostic: state of the photons the watchdog abandoned, 16 doubles each: id, n_step, phase, depth,
+ * pend, w, e_0_s, dl, x[4], k[4].  out holds cap records; returns the records kept (<= 256). */
+int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap);
 
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
 /* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */

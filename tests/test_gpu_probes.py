@@ -126,7 +126,7 @@ def test_fluid_and_radiation(engine, oracle64, samples):
     O, L = _o()
     _, x, k = samples
     fl = engine.probe(4, x, 19)
-    rad = engine.probe(5, np.concatenate([x, k], axis=1), 4)
+    rad = engine.probe(5, np.concatenate([x, k], axis=1), 6)
     b_unit = oracle64.units.b_unit
     for i in range(len(x)):
         f = np.zeros(1, dtype=O.FLUID)
@@ -140,7 +140,9 @@ def test_fluid_and_radiation(engine, oracle64, samples):
         a_s = L.grmo_alpha_inv_scatt(oracle64.h, nu, f["theta_e"][0], f["n_e"][0])
         a_a = L.grmo_alpha_inv_abs(oracle64.h, nu, f["theta_e"][0], f["n_e"][0], f["b"][0], th)
         np.testing.assert_allclose(rad[i, :2], [th, nu], rtol=1e-9, atol=1e-12)
-        np.testing.assert_allclose(rad[i, 2:], [a_s, a_a], rtol=1e-9, atol=1e-300)
+        np.testing.assert_allclose(rad[i, 2:4], [a_s, a_a], rtol=1e-9, atol=1e-300)
+    # the fused evaluation the transport step uses (radiation_coeffs) against the separate functions
+    np.testing.assert_allclose(rad[:, 2:4], rad[:, 4:6], rtol=1e-12, atol=1e-300)
 
 
 def test_hotcross_and_synch(engine, oracle64):

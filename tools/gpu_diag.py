@@ -26,6 +26,7 @@ if grid:
 if os.environ.get("WARMUP"):
     e.set_option(G.OPT_WARMUP, int(os.environ["WARMUP"]))
     print(f"warmup {os.environ['WARMUP']}", flush=True)
+e.set_option(G.OPT_WATCHDOG_MS, int(os.environ.get("WATCHDOG_MS", "60000")))
 if os.environ.get("REFILL_MIN"):
     e.set_option(G.OPT_REFILL_MIN, int(os.environ["REFILL_MIN"]))
     print(f"refill_min {os.environ['REFILL_MIN']}", flush=True)
@@ -39,11 +40,18 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
     if os.environ.get("SEED"):
         e.set_option(G.OPT_SEED, int(os.environ["SEED"]) + rep)
     t = time.time()
-    if dev_emit:
-        p, n_dev = e.emit(seed=123)
-        e.track_device(p, n_dev)
-    else:
-        e.track(ph)
+    try:
+        if dev_emit:
+            p, n_dev = e.emit(seed=123)
+            e.track_device(p, n_dev)
+        else:
+            e.track(ph)
+    except RuntimeError as exc:
+        print(f"rep {rep}: FAILED after {time.time() - t:.1f}s: {exc}", flush=True)
+        np.set_printoptions(linewidth=200, precision=6)
+        print("stuck: id n_step phase depth pend w e_0_s dl x0..3 k0..3", flush=True)
+        print(e.debug_stuck()[:16], flush=True)
+        sys.exit(3)
     wall = time.time() - t
     spec, nr, ns, mt = e.finish()
     st = e.stats()
@@ -52,7 +60,7 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
           f"children {st['n_children']} overflow {st['n_overflow']} launches {st['n_launches']} "
           f"rate {len(ph) / (st['last_kernel_ms'] * 1e-3):.4g} ph/s rec {nr} scatt {ns} | longest launch "
           f"{st['max_launch_ms']:.1f}ms ({st['max_launch_steps']} steps) longest life {st['max_photon_steps']} steps, "
-          f"{st['n_long_photons']} lives > 1e5 steps", flush=True)
+          f"{st['n_long_photons']} lives > 1e5 steps, {st['n_nan_photons']} NaN-ended", flush=True)
     wv = e.debug_waves().astype(np.float64)
     t0w = wv[:, 0].min()
     ex = (wv[:, 1] - t0w) / 1e5  # ms

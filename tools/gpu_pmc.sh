@@ -11,6 +11,7 @@ SETS=(
   "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH"
   "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum"
 )
+if [ -n "$PMC_SETS" ]; then IFS=';' read -r -a SETS <<< "$PMC_SETS"; fi
 i=0
 for set in "${SETS[@]}"; do
   i=$((i+1))
