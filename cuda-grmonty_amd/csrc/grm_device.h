@@ -95,8 +95,10 @@ __device__ __forceinline__ void philox_block(uint32_t c0, uint32_t c1, uint32_t 
                                              uint32_t k1, uint32_t &o0, uint32_t &o1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        /* one 32x32->64 multiply (v_mad_u64_u32) per product instead of mul_lo + mul_hi */
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         const uint32_t n0 = hi1 ^ c1 ^ k0;
         const uint32_t n2 = hi0 ^ c3 ^ k1;
         c0 = n0;
@@ -696,9 +698,9 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
     const double nu_s = (2.0 / 9.0) * nu_c * theta_e * theta_e * sin_theta;
     const double x = fdiv(nu, nu_s);
     const double xp = cbrt(x);
-    const double xx = sqrt(x) + JNU_CST * sqrt(xp);
+    const double sxp = sqrt(xp);
+    const double xx = xp * sxp + JNU_CST * sxp; /* sqrt(x) = xp^(3/2) */
     const double f = xx * xx;
-    const double ex = exp(-xp);
     const double xb = fdiv(w, theta_e);
     double b_nu;
     if (xb < 1.0e-3)
@@ -723,14 +725,16 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
     /* absorption: j_nu / nu^2 / (B_nu / nu^3) */
     double jnu = 0.0;
     if (!(theta_e < THETA_E_MIN) && !(nu > 1.0e12 * nu_s)) {
-        double k2;
+        /* exp(-x^(1/3)) / K2 as one exponential: K2 = exp(table lerp), or 2 theta_e^2 above the
+         * table (then through log -- rare) */
+        double l_k2;
         if (theta_e > JNU_MAX_T) {
-            k2 = 2.0 * theta_e * theta_e;
+            l_k2 = log(2.0 * theta_e * theta_e);
         } else {
             dk -= ik;
-            k2 = exp((1.0 - dk) * k2a + dk * k2b);
+            l_k2 = (1.0 - dk) * k2a + dk * k2b;
         }
-        jnu = fdiv((kSqrt2 * kPi * EE * EE / (3.0 * CL)) * n_e * nu_s, k2) * f * ex;
+        jnu = ((kSqrt2 * kPi * EE * EE / (3.0 * CL)) * n_e * nu_s) * f * exp(-xp - l_k2);
     }
     a_a = fdiv(jnu, nu * nu * (b_nu + 1.0e-100));
 }

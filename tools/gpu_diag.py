@@ -68,7 +68,8 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
     q = np.percentile(ex, [0, 10, 50, 90, 99, 100])
     print(f"  waves {len(wv)}: start max {st_.max():.2f}ms, exit ms p0/10/50/90/99/100 "
           + "/".join(f"{v:.0f}" for v in q) + f", trips max/median {wv[:, 2].max():.0f}/{np.median(wv[:, 2]):.0f}, "
-          f"photons max/median {wv[:, 3].max():.0f}/{np.median(wv[:, 3]):.0f}", flush=True)
+          f"photons max/median {wv[:, 3].max():.0f}/{np.median(wv[:, 3]):.0f}, "
+          f"bulk {st['last_steps'] / max(q[2], 1e-9) / 1e3:.4g} Msteps/s (steps / median wave exit)", flush=True)
     inst, tm = e.debug_timing(reset=True)
     if inst:
         tot = max(tm[3], 1)
