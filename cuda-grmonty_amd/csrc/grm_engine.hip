@@ -47,6 +47,14 @@ namespace {
 #ifndef GRM_WAVES_PER_SIMD
 #define GRM_WAVES_PER_SIMD (GRM_BLOCK / 256)
 #endif
+/* 256 lanes per CU: spectrum in LDS.  512 lanes (two waves per SIMD): the LDS state copies take
+ * 90 KB, so the spectrum goes to a per-workgroup slice in HBM (L2 atomics).
+ * GRM_PREFETCH=1 issues the fluid gather during the push (its 64 VGPRs held across the connection
+ * and corrector); measured 2.5% slower than gathering at the use at one wave per SIMD. */
+#define GRM_SPEC_LDS (GRM_BLOCK <= 256)
+#ifndef GRM_PREFETCH
+#define GRM_PREFETCH 0
+#endif
 constexpr int BLOCK = GRM_BLOCK;
 constexpr int MIN_WAVES_PER_SIMD = GRM_WAVES_PER_SIMD;
 constexpr int STACK_DEPTH = 16;                 /* scatter-request slots per lane ... */
@@ -94,6 +102,7 @@ struct Ctl {
     unsigned long long ovf_cap;
     unsigned long long *ovf_count;
     grm_spectrum_cell *spec;
+    double *spec_blocks;   /* [grid][SPEC_LDS] per-workgroup spectrum slices (when not in LDS), kept zero */
     DevCounters *ctr;
     grm_trace *trace;
     unsigned long long trace_cap;
@@ -120,11 +129,24 @@ struct Ctl {
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 
-/* hot photon state: lives in VGPRs for the photon's whole life */
+/* Per-step (or rarer) lane fields: registers in the one-wave build; in the two-wave build
+ * (GRM_LANE_LDS) an LDS column per lane ([field][lane], conflict-free), read and written where used
+ * -- what brings the kernel's register demand under the 256 VGPRs two waves per SIMD allow. */
+#ifndef GRM_LANE_LDS
+#define GRM_LANE_LDS (GRM_BLOCK > 256)
+#endif
+#define GRM_LANE_XFIELDS(X)                                                                          \
+    X(tau_abs, 0) X(tau_scatt, 1) X(alpha_scatti, 2) X(alpha_absi, 3) X(bi, 4) X(fl_ne, 5)          \
+    X(ph2_x0, 6)      /* photon_2's x^0 (the rest of it is in the ph2 LDS slot) */                  \
+    X(ph2_e0s, 7)     /* photon_2's e_0_s */                                                          \
+    X(bk_x0, 8)       /* x^0 of the halving backup (the rest of it is in the bk LDS slot) */          \
+    X(p_dtau_abs, 9) X(p_dtau_scatt, 10) X(p_wc, 11) /* carried across the re-push */
+constexpr int LANE_XFIELDS = 12;
+
+/* hot photon state: lives in VGPRs (and, see above, LDS) for the photon's whole life */
 struct Lane {
     double x[4], k[4], dk[4];
-    double w, e_0_s, tau_abs, tau_scatt;
-    double alpha_scatti, alpha_absi, bi, fl_ne;
+    double w, e_0_s;
     int n_scatt, n_step;
     int flight;                           /* warm-up: photons started (+) / ended (-) since the last flush */
     Rng rng;
@@ -133,9 +155,18 @@ struct Lane {
     int phase, depth;
     uint32_t pend;
     double dl, hlen;                      /* step size of this iteration; length being pushed */
-    double ph2_x0, ph2_e0s;               /* photon_2's x^0 and e_0_s (the rest of it is in LDS) */
-    double bk_x0;                         /* x^0 of the halving backup (the rest of it is in LDS) */
-    double p_dtau_abs, p_dtau_scatt, p_wc; /* carried across the re-push */
+#if GRM_LANE_LDS
+    volatile double *xs;                  /* this lane's LDS column */
+#define X(name, i) \
+    __device__ __forceinline__ volatile double &name() const { return xs[(i) * GRM_BLOCK]; }
+#else
+    double xf[LANE_XFIELDS];
+#define X(name, i)                                                           \
+    __device__ __forceinline__ double &name() { return xf[i]; }              \
+    __device__ __forceinline__ double name() const { return xf[i]; }
+#endif
+    GRM_LANE_XFIELDS(X)
+#undef X
 };
 
 /* Denominator of bias_func's first term, bias_norm * max_tau_scatt * (<N_scatt> + 2)
@@ -242,7 +273,7 @@ __device__ void write_trace(const Ctl &C, const Cold *cold, uint64_t id, double 
 
 __device__ __forceinline__ void trace_end(const Ctl &C, const Cold *cold, const Lane &L, int reason) {
     if (C.trace)
-        write_trace(C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs, L.tau_scatt, L.n_scatt, L.n_step,
+        write_trace(C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt, L.n_step,
                     reason, -1, -1);
 }
 
@@ -254,7 +285,12 @@ __device__ __forceinline__ void trace_end(const Ctl &C, const Cold *cold, const 
  * Field f of a cell = field f of grm_spectrum_cell (e_0, never accumulated, is left out). */
 constexpr int SPEC_FIELDS = 12;
 constexpr int SPEC_LDS = N_TH_BINS * N_E_BINS * SPEC_FIELDS;
+#if GRM_SPEC_LDS
 __shared__ double s_spec[SPEC_LDS];
+__device__ __forceinline__ double *spec_slice(const Ctl &) { return s_spec; }
+#else
+__device__ __forceinline__ double *spec_slice(const Ctl &C) { return C.spec_blocks + (size_t)blockIdx.x * SPEC_LDS; }
+#endif
 __shared__ unsigned long long s_cnt[BLOCK / 64][4]; /* n_recorded, n_scatt, max tau bits, max flushed */
 
 __device__ __forceinline__ void flush_counters(const Ctl &C) {
@@ -293,7 +329,7 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
                 reason = 0;
                 atomicAdd(cnt + 0, 1ull);
                 atomicAdd(cnt + 1, (unsigned long long)n_scatt);
-                double *s = s_spec + (ix2 * N_E_BINS + i_e) * SPEC_FIELDS;
+                double *s = spec_slice(C) + (ix2 * N_E_BINS + i_e) * SPEC_FIELDS;
                 const double x1i = cold->x1i, x2i = cold->x2i;
                 atomicAdd(s + 0, w);                      /* dn_dle */
                 atomicAdd(s + 1, w * e);                  /* de_dle */
@@ -321,37 +357,9 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
 __device__ __forceinline__ void end_of_life(const Params &P, const Ctl &C, const Cold *cold, const Lane &L) {
     /* record_criterion (harm_model.cpp:1618) && n_step <= max_n_step (:1066) */
     if (L.x[1] > P.x1_max && L.n_step <= MAX_N_STEP)
-        record_photon(P, C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs, L.tau_scatt, L.n_scatt, L.n_step);
+        record_photon(P, C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt, L.n_step);
     else
         trace_end(C, cold, L, 2);
-}
-
-/* photon set-up at the head of track_super_photon (harm_model.cpp:895-917). false = invalid */
-__device__ bool init_photon(const Params &P, const Ctl &C, const Cold *cold, Lane &L, double bias_d) {
-    if (isnan(L.x[0]) || isnan(L.x[1]) || isnan(L.x[2]) || isnan(L.x[3]) || isnan(L.k[0]) || isnan(L.k[1]) ||
-        isnan(L.k[2]) || isnan(L.k[3]) || L.w == 0.0) {
-        trace_end(C, cold, L, 4);
-        return false;
-    }
-    Trig T;
-    trig_at(P, L.x, T);
-    Gcov G;
-    gcov_from_trig(P, T, G);
-    Fluid F;
-    fluid_params(P, L.x, G, F);
-    const double nu = fluid_nu(L.k, F);
-    radiation_coeffs(P, L.k, F, nu, L.alpha_scatti, L.alpha_absi);
-    L.bi = bias_func(bias_d, F.theta_e, L.w);
-    L.fl_ne = F.n_e;
-    Conn Cn;
-    connection(P, T, Cn);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) L.dk[i] = geo_rhs(Cn, i, L.k);
-    L.n_step = 0;
-    L.tau_abs = L.tau_scatt = 0.0;
-    L.e_0_s = cold->e;
-    L.phase = 0;
-    return true;
 }
 
 /* emitted photon -> lane (harm_model.cpp:373-391) */
@@ -531,14 +539,38 @@ __device__ __forceinline__ void load_xkdk(const Slot &s, Lane &L) {
 }
 
 __device__ __forceinline__ void store_ph2(const Slot &ph2, Lane &L) {
-    L.ph2_x0 = L.x[0];
-    L.ph2_e0s = L.e_0_s;
+    L.ph2_x0() = L.x[0];
+    L.ph2_e0s() = L.e_0_s;
     save_xkdk(ph2, L);
 }
 
 __device__ __forceinline__ void load_ph2(const Slot &ph2, Lane &L) {
-    L.x[0] = L.ph2_x0;
+    L.x[0] = L.ph2_x0();
     load_xkdk(ph2, L);
+}
+
+/* photon set-up at the head of track_super_photon (harm_model.cpp:895-917).  Here only the validity
+ * check and the counters; the rest -- fluid and absorption/scattering coefficients at x, bias, and
+ * dk/dlambda from the connection at x (init_dkdlam) -- runs on the lane's next trip as phase 3,
+ * inside the same push and fluid/radiation code the stepping lanes execute (see transport_trip), so
+ * a refill costs a few loads instead of a divergent block of its own.  false = invalid. */
+__device__ bool init_photon(const Ctl &C, const Cold *cold, Lane &L, const Slot &ph2) {
+    if (isnan(L.x[0]) || isnan(L.x[1]) || isnan(L.x[2]) || isnan(L.x[3]) || isnan(L.k[0]) || isnan(L.k[1]) ||
+        isnan(L.k[2]) || isnan(L.k[3]) || L.w == 0.0) {
+        trace_end(C, cold, L, 4);
+        return false;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L.dk[i] = 0.0;
+    store_ph2(ph2, L); /* x, k kept here across the set-up's zero-length push */
+    L.n_step = 0;
+    L.tau_abs() = L.tau_scatt() = 0.0;
+    L.e_0_s = cold->e;
+    L.hlen = 0.0;
+    L.depth = 0;
+    L.pend = 0;
+    L.phase = 3;
+    return true;
 }
 
 /* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
@@ -547,7 +579,7 @@ __device__ __forceinline__ void load_ph2(const Slot &ph2, Lane &L) {
  * :1279-1285) spends extra trips while the other lanes of the wave keep stepping, instead of the
  * whole wave waiting for the deepest halving tree.  Returns false when the photon's life ended. */
 __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *wstack, int *wtop,
-                               unsigned long long &steps, unsigned long long &children, const Slot &ph2,
+                               unsigned &steps, unsigned &children, const Slot &ph2,
                                const Slot &bk, double bias_d) {
     if (L.phase == 0) {
         if (stop_criterion(P, L)) {
@@ -563,32 +595,46 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         L.phase = 1;
     }
     TSTAMP(8);
-    /* one attempt of push_photon at the current node of the halving tree (:1217-1289) */
+    /* one attempt of push_photon at the current node of the halving tree (:1217-1289).  A lane in
+     * set-up (phase 3) makes a zero-length attempt instead: x and k stay, the corrector's first pass
+     * leaves dk = dk/dlambda from the connection at x -- init_dkdlam (:915, :1571-1587) -- and T, G
+     * are then at x for the fluid evaluation below. */
+    const bool setup = L.phase == 3;
     Trig T;
     Gcov G;
     ZoneFetch Z;
     bool have_tg = false;
-    if (!(L.x[1] < P.xs1)) {
+    if (setup || !(L.x[1] < P.xs1)) {
         if (L.depth > 0) {
-            L.bk_x0 = L.x[0];
+            L.bk_x0() = L.x[0];
             save_xkdk(bk, L);
         }
         double e_1;
         const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -L.depth), e_1, T, G,
+#if GRM_PREFETCH
                                        [&](const double *xn) { zone_fetch(P, xn, Z); });
+#else
+                                       NoPrefetch());
+#endif
         TSTAMP(9);
-        if (fail && L.depth < MAX_SUBDIV) {
+        if (setup) {
+            /* restore x, k exactly (a non-finite dk must not leak into them through 0 * dk) */
+#pragma unroll
+            for (int i = 0; i < 3; ++i) L.x[1 + i] = ph2[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) L.k[i] = ph2[3 + i];
+        } else if (fail && L.depth < MAX_SUBDIV) {
             if (L.depth == 0) {
                 load_ph2(ph2, L);
             } else {
-                L.x[0] = L.bk_x0;
+                L.x[0] = L.bk_x0();
                 load_xkdk(bk, L);
             }
             ++L.depth;
             L.pend |= 1u << L.depth;
             return true;
         }
-        L.e_0_s = e_1;
+        if (!setup) L.e_0_s = e_1;
         have_tg = true;
     }
     if (L.pend) {
@@ -601,7 +647,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
      * Both evaluate the fluid and the absorption/scattering coefficients at the new point; they share
      * ONE evaluation here so a wave with lanes in both phases runs that code once. */
     const bool at_scatter = L.phase == 2;
-    if (!at_scatter) {
+    if (!at_scatter && !setup) {
         ++steps;
         if (stop_criterion(P, L)) {
             end_of_life(P, C, cold, L);
@@ -619,15 +665,20 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         }
     }
     TSTAMP(10);
-    if (at_scatter || L.alpha_absi > 0.0 || L.alpha_scatti > 0.0 || L.fl_ne > 0.0) {
+    if (setup || at_scatter || L.alpha_absi() > 0.0 || L.alpha_scatti() > 0.0 || L.fl_ne() > 0.0) {
         if (!have_tg) {
             trig_at(P, L.x, T);
             gcov_from_trig(P, T, G);
+#if GRM_PREFETCH
             zone_fetch(P, L.x, Z);
+#endif
         }
+#if !GRM_PREFETCH
+        zone_fetch(P, L.x, Z);
+#endif
         Fluid F;
         fluid_from(P, L.x, G, Z, F);
-        L.fl_ne = F.n_e;
+        L.fl_ne() = F.n_e;
         TSTAMP(11);
         /* scatter_super_photon's parent-side check (:1076-1081) */
         if (at_scatter && F.n_e > 0.0 &&
@@ -640,41 +691,48 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         /* phase 1 skips the coefficients out of the fluid (bound_flag, :941-955); both skip them
          * for nu < 0 */
         const double nu = fluid_nu(L.k, F);
-        const bool zero = nu < 0.0 || (!at_scatter && F.n_e == 0.0);
+        const bool zero = !setup && (nu < 0.0 || (!at_scatter && F.n_e == 0.0));
         double a_s = 0.0, a_a = 0.0;
         if (!zero) {
             radiation_coeffs(P, L.k, F, nu, a_s, a_a);
         }
         const double bf = (zero && !at_scatter) ? 0.0 : bias_func(bias_d, F.theta_e, L.w);
         TSTAMP(12);
+        if (setup) { /* the set-up's coefficients (:905-913); the loop starts on the next trip */
+            L.alpha_scatti() = a_s;
+            L.alpha_absi() = a_a;
+            L.bi() = bf;
+            L.phase = 0;
+            return true;
+        }
         if (at_scatter) {
             /* the child leaves as a scatter request; its stores go out after this trip's table
              * loads, so no load of the trip waits behind them (vmcnt is in order) */
             if (F.n_e > 0.0) {
-                if (push_request(C, L, cold, F, L.p_wc, wstack, wtop)) ++L.flight;
+                if (push_request(C, L, cold, F, L.p_wc(), wstack, wtop)) ++L.flight;
                 ++children;
             }
-            L.alpha_scatti = a_s;
-            L.alpha_absi = a_a;
-            L.bi = bf;
-            L.tau_abs += L.p_dtau_abs;
-            L.tau_scatt += L.p_dtau_scatt;
+            L.alpha_scatti() = a_s;
+            L.alpha_absi() = a_a;
+            L.bi() = bf;
+            L.tau_abs() += L.p_dtau_abs();
+            L.tau_scatt() += L.p_dtau_scatt();
         } else {
             /* trapezoid optical depths over the step (:957-975) */
             const double dl = L.dl;
             double d_tau_scatt, d_tau_abs, bias;
             if (zero) {
-                d_tau_scatt = 0.5 * L.alpha_scatti * P.d_tau_k * dl;
-                d_tau_abs = 0.5 * L.alpha_absi * P.d_tau_k * dl;
+                d_tau_scatt = 0.5 * L.alpha_scatti() * P.d_tau_k * dl;
+                d_tau_abs = 0.5 * L.alpha_absi() * P.d_tau_k * dl;
                 bias = 0.0;
             } else {
-                d_tau_scatt = 0.5 * (L.alpha_scatti + a_s) * P.d_tau_k * dl;
-                d_tau_abs = 0.5 * (L.alpha_absi + a_a) * P.d_tau_k * dl;
-                bias = 0.5 * (L.bi + bf);
+                d_tau_scatt = 0.5 * (L.alpha_scatti() + a_s) * P.d_tau_k * dl;
+                d_tau_abs = 0.5 * (L.alpha_absi() + a_a) * P.d_tau_k * dl;
+                bias = 0.5 * (L.bi() + bf);
             }
-            L.alpha_scatti = a_s;
-            L.alpha_absi = a_a;
-            L.bi = bf;
+            L.alpha_scatti() = a_s;
+            L.alpha_absi() = a_a;
+            L.bi() = bf;
             const double x1 = -log(uniform(L.rng));
             const double wc = fdiv(L.w, bias);
             if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) {
@@ -692,14 +750,14 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
                     L.w *= exp(-d_tau);
                 /* re-push photon_2 by dl*frac to the scattering point (:1005), on later trips */
                 load_ph2(ph2, L);
-                L.e_0_s = L.ph2_e0s;
+                L.e_0_s = L.ph2_e0s();
                 L.hlen = dl * frac;
                 L.depth = 0;
                 L.pend = 0;
                 L.phase = 2;
-                L.p_dtau_abs = d_tau_abs;
-                L.p_dtau_scatt = d_tau_scatt;
-                L.p_wc = wc;
+                L.p_dtau_abs() = d_tau_abs;
+                L.p_dtau_scatt() = d_tau_scatt;
+                L.p_wc() = wc;
                 return true;
             }
             if (d_tau_abs > 100) {
@@ -711,8 +769,8 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
                 L.w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
             else
                 L.w *= exp(-d_tau);
-            L.tau_abs += d_tau_abs;
-            L.tau_scatt += d_tau_scatt;
+            L.tau_abs() += d_tau_abs;
+            L.tau_scatt() += d_tau_scatt;
         }
     }
     TSTAMP(13);
@@ -749,7 +807,11 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) < 16) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
 #endif
+#if GRM_LANE_LDS
+    __shared__ double lds[(2 * LDS_DOUBLES_PER_LANE + LANE_XFIELDS) * BLOCK];
+#else
     __shared__ double lds[2 * LDS_DOUBLES_PER_LANE * BLOCK];
+#endif
     const Slot ph2{lds + threadIdx.x, BLOCK};
     const Slot bk{lds + LDS_DOUBLES_PER_LANE * BLOCK + threadIdx.x, BLOCK};
     const unsigned lane_id = threadIdx.x & 63;
@@ -759,13 +821,18 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     __shared__ int s_wtop[BLOCK / 64];
     int *wtop = s_wtop + wave;
     if (lane_id == 0) *wtop = 0;
+#if GRM_SPEC_LDS
     for (int i = threadIdx.x; i < SPEC_LDS; i += BLOCK) s_spec[i] = 0.0;
+#endif
     if (lane_id < 4) s_cnt[wave][lane_id] = 0;
     __syncthreads();
     Cold *cold = C.cold + gtid;
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long wave_trips = 0;
     Lane L;
+#if GRM_LANE_LDS
+    L.xs = lds + 2 * LDS_DOUBLES_PER_LANE * BLOCK + threadIdx.x;
+#endif
     L.rng.k0 = C.key0;
     L.rng.k1 = C.key1;
     bool active = false;
@@ -775,8 +842,10 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     L.flight = 0;
     double bias_d = bias_den(P, C); /* wave-uniform, refreshed every 16 trips when live */
     unsigned trip = 1;
-    unsigned long long steps = 0, tracked = 0, primaries = 0, children = 0;
-    unsigned long long nstep_max = 0, n_long = 0; /* longest photon life; lives > 100k steps */
+    /* per-lane launch counters, 32-bit in the loop (a lane makes < 2^32 steps per launch), widened
+     * for the wave reduction at exit */
+    unsigned steps = 0, tracked = 0, primaries = 0, children = 0;
+    unsigned nstep_max = 0, n_long = 0; /* longest photon life; lives > 100k steps */
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
 
     while (true) {
@@ -902,7 +971,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 }
                 if (has) {
                     ++tracked;
-                    if (ok) active = init_photon(P, C, cold, L, bias_d);
+                    if (ok) active = init_photon(C, cold, L, ph2);
                     if (!active) --L.flight; /* started and ended at once (invalid) */
                 }
                 TSTAMP(1);
@@ -930,7 +999,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         if (active) {
             active = transport_trip(P, C, L, cold, wstack, wtop, steps, children, ph2, bk, bias_d);
             if (!active) {
-                nstep_max = max(nstep_max, (unsigned long long)L.n_step);
+                nstep_max = max(nstep_max, (unsigned)L.n_step);
                 n_long += L.n_step > 100000 ? 1 : 0;
                 --L.flight;
             }
@@ -953,27 +1022,36 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     /* counters, then the workgroup's spectrum, to the global accumulators */
     flush_counters(C);
     __syncthreads();
+    double *slice = spec_slice(C);
     for (int i = threadIdx.x; i < SPEC_LDS; i += BLOCK) {
-        const double v = s_spec[i];
+#if GRM_SPEC_LDS
+        const double v = slice[i];
+#else
+        /* the slice was accumulated by L2 atomics; read it there and leave it zero for the next launch */
+        const double v = __hip_atomic_load(slice + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v != 0.0) slice[i] = 0.0;
+#endif
         if (v != 0.0) unsafeAtomicAdd(reinterpret_cast<double *>(C.spec + i / SPEC_FIELDS) + i % SPEC_FIELDS, v);
     }
     /* wave-reduce the lane counters, one atomic per wave */
+    unsigned long long w_steps = steps, w_tracked = tracked, w_primaries = primaries, w_children = children;
+    unsigned long long w_long = n_long, w_nstep_max = nstep_max;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        steps += __shfl_xor(steps, off);
-        tracked += __shfl_xor(tracked, off);
-        primaries += __shfl_xor(primaries, off);
-        children += __shfl_xor(children, off);
-        n_long += __shfl_xor(n_long, off);
-        nstep_max = max(nstep_max, (unsigned long long)__shfl_xor(nstep_max, off));
+        w_steps += __shfl_xor(w_steps, off);
+        w_tracked += __shfl_xor(w_tracked, off);
+        w_primaries += __shfl_xor(w_primaries, off);
+        w_children += __shfl_xor(w_children, off);
+        w_long += __shfl_xor(w_long, off);
+        w_nstep_max = max(w_nstep_max, (unsigned long long)__shfl_xor(w_nstep_max, off));
     }
     if (lane_id == 0) {
-        atomicAdd(&C.ctr->n_steps, steps);
-        atomicAdd(&C.ctr->n_tracked, tracked);
-        atomicAdd(&C.ctr->n_primaries, primaries);
-        atomicAdd(&C.ctr->n_children, children);
-        if (n_long) atomicAdd(&C.ctr->n_long, n_long);
-        atomicMax(&C.ctr->max_nstep, nstep_max);
+        atomicAdd(&C.ctr->n_steps, w_steps);
+        atomicAdd(&C.ctr->n_tracked, w_tracked);
+        atomicAdd(&C.ctr->n_primaries, w_primaries);
+        atomicAdd(&C.ctr->n_children, w_children);
+        if (w_long) atomicAdd(&C.ctr->n_long, w_long);
+        atomicMax(&C.ctr->max_nstep, w_nstep_max);
         unsigned long long *wr = C.waves + (gtid >> 6) * 4;
         wr[0] = rt_start;
         wr[1] = __builtin_amdgcn_s_memrealtime();
@@ -1015,7 +1093,7 @@ struct grm_engine {
     double max_tau_init = 0.0;
     bool frozen_set = false;
     int64_t warmup = -1;     /* photons; -1 = lanes */
-    int refill_min = 16;
+    int refill_min = 2;      /* measured: 16 -> 2 is +4% once the set-up moved into the trip (phase 3) */
     uint64_t history = 0;    /* primaries tracked since reset */
     double fz_scatt = 0.0, fz_rec = 0.0, fz_maxtau = 0.0;
     grm_stats stats{};
@@ -1026,6 +1104,7 @@ struct grm_engine {
     unsigned long long *d_waves = nullptr; /* [lanes / 64][4] per-wave record of the last launch */
     int64_t watchdog_ms = 60000;           /* per-launch watchdog (GRM_OPT_WATCHDOG_MS; 0 = off) */
     double *d_stuck = nullptr;             /* [STUCK_CAP][STUCK_WORDS] abandoned-photon records */
+    double *d_spec_blocks = nullptr;       /* per-workgroup spectrum slices (GRM_SPEC_LDS == 0) */
     /* device emission: zone table, emission tables, zone offsets, emitted photons */
     grm_emit_zone *d_ezones = nullptr;
     double *d_eweight = nullptr, *d_ef = nullptr;
@@ -1068,6 +1147,12 @@ int alloc_lanes(grm_engine *e) {
         if (e->d_waves) (void)hipFree(e->d_waves);
         e->d_waves = nullptr;
         HIPCHK(e, hipMalloc(&e->d_waves, lanes / 64 * 4 * sizeof(unsigned long long)));
+#if !GRM_SPEC_LDS
+        if (e->d_spec_blocks) (void)hipFree(e->d_spec_blocks);
+        e->d_spec_blocks = nullptr;
+        HIPCHK(e, hipMalloc(&e->d_spec_blocks, (size_t)grid * SPEC_LDS * sizeof(double)));
+        HIPCHK(e, hipMemset(e->d_spec_blocks, 0, (size_t)grid * SPEC_LDS * sizeof(double)));
+#endif
         e->lanes = lanes;
     }
     e->grid = grid;
@@ -1101,6 +1186,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     C.cold = e->d_cold;
     C.ovf_cap = e->ovf_cap;
     C.spec = e->d_spec;
+    C.spec_blocks = e->d_spec_blocks;
     C.ctr = e->d_ctr;
     C.trace = e->trace_cap ? e->d_trace : nullptr;
     C.trace_cap = e->trace_cap;
@@ -1340,6 +1426,7 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_ovf[1]);
     hipFree(e->d_small);
     hipFree(e->d_stuck);
+    hipFree(e->d_spec_blocks);
     hipFree(e->d_batch);
     hipFree(e->d_trace);
     hipFree(e->d_upload);

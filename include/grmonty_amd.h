@@ -136,7 +136,7 @@ enum {
      * batch is cut into launches that double the history each time, so the adaptive bias
      * counters evolve as in the serial reference (-1 = one persistent grid's worth of lanes, 0 = off) */
     GRM_OPT_WARMUP = 8,
-    /* idle lanes a wavefront gathers before it refills them together (1..64, default 16):
+    /* idle lanes a wavefront gathers before it refills them together (1..64, default 2):
      * larger = less divergent child sampling / photon set-up, more idle lane-trips */
     GRM_OPT_REFILL_MIN = 9,
     /* per-launch watchdog in ms (default 60000, 0 = off): a transport launch running longer abandons
