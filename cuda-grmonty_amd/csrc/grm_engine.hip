@@ -110,7 +110,8 @@ struct Ctl {
     int bias_frozen;
     double f_scatt, f_rec, f_maxtau;
     unsigned long long *timing; /* GRM_TIMING builds: per-region wave cycles */
-    int refill_min;             /* idle lanes a wave gathers before it refills (batching) */
+    int refill_min;             /* idle lanes a wave gathers before it takes primaries */
+    int child_min;              /* children a wave gathers (on its stack and idle lanes) per sampling batch */
     /* Live-bias warm-up inside the launch: the first admit_n pool photons go in batches, each
      * admitted only when everything started before it (children included) has ended, and as large
      * as the history behind it (64, 64, 128, 256, ...): bias_func's running counters then evolve as
@@ -873,21 +874,31 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             }
             TSTAMP(7);
         }
-        /* Batched refill (converged point).  Idle lanes wait until at least refill_min of them can
-         * be refilled together -- children from the wave's stack first (depth-first order, like the
-         * reference's recursion, harm_model.cpp:1023), then primaries from the shared pool -- so the
-         * divergent child sampling and the photon set-up run once for a group of lanes instead of
-         * once per lane.  With no lane active, or once the pool is drained and every waiting child
-         * fits, the wave refills whatever it can. */
+        /* Refill (converged point).  A primary needs only its loads here (its set-up runs in the
+         * trip, phase 3), so idle lanes take primaries as soon as refill_min of them are idle.  A
+         * child needs the divergent scattering sampling (sample_child), so children go in batches:
+         * once child_min wait on the wave's stack, the wave stops taking primaries until as many
+         * lanes are idle and samples them together (stack order: depth-first, like the reference's
+         * recursion, harm_model.cpp:1023).  With no lane active, or once the pool is drained, the
+         * wave refills whatever it can. */
         const unsigned long long idle = __ballot(!active);
         if (idle) {
             int top = *wtop;
             if (top > WSTACK_CAP) top = WSTACK_CAP;
             const int n_idle = __popcll(idle);
-            const int k_child = n_idle < top ? n_idle : top;
-            int k_pool = pool_done ? 0 : n_idle - k_child;
             const bool none_active = idle == __ballot(1);
-            if (k_child + k_pool >= C.refill_min || none_active || (pool_done && top > 0 && top <= n_idle)) {
+            const bool child_due = top >= C.child_min || (pool_done && top > 0);
+            int k_child = 0, k_pool = 0;
+            bool go;
+            if (none_active || child_due) {
+                k_child = n_idle < top ? n_idle : top;
+                k_pool = pool_done ? 0 : n_idle - k_child;
+                go = none_active || n_idle >= min(C.child_min, top);
+            } else {
+                k_pool = pool_done ? 0 : n_idle;
+                go = k_pool >= C.refill_min;
+            }
+            if (go) {
                 const int r = __popcll(idle & lt_mask);
                 unsigned long long base = 0;
                 if (k_pool > 0) {
@@ -1093,7 +1104,8 @@ struct grm_engine {
     double max_tau_init = 0.0;
     bool frozen_set = false;
     int64_t warmup = -1;     /* photons; -1 = lanes */
-    int refill_min = 2;      /* measured: 16 -> 2 is +4% once the set-up moved into the trip (phase 3) */
+    int refill_min = 2;      /* primaries: set-up is in the trip (phase 3), so refill early */
+    int child_min = 8;       /* children: batch the divergent scattering sampling */
     uint64_t history = 0;    /* primaries tracked since reset */
     double fz_scatt = 0.0, fz_rec = 0.0, fz_maxtau = 0.0;
     grm_stats stats{};
@@ -1194,6 +1206,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     C.timing = e->d_timing;
     C.waves = e->d_waves;
     C.refill_min = e->refill_min;
+    C.child_min = e->child_min;
     C.lanes = (int)e->lanes;
     C.bias_frozen = e->bias_mode;
     C.in_flight = e->d_small + 4;
@@ -1468,6 +1481,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_FROZEN_MAXTAU: std::memcpy(&e->fz_maxtau, &v, sizeof(double)); e->frozen_set = true; return 0;
     case GRM_OPT_WARMUP: e->warmup = v; return 0;
     case GRM_OPT_REFILL_MIN: e->refill_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
+    case GRM_OPT_CHILD_MIN: e->child_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }

@@ -46,6 +46,7 @@ EMIT_ZONE = np.dtype([("nz", "<f8"), ("dn_max", "<f8"), ("x", "<f8", 4), ("n_e",
 OPT_SEED, OPT_BIAS_MODE, OPT_TRACE_CAP, OPT_GRID_BLOCKS, OPT_ID_BASE = 0, 1, 2, 3, 4
 OPT_FROZEN_SCATT, OPT_FROZEN_REC, OPT_FROZEN_MAXTAU, OPT_WARMUP, OPT_REFILL_MIN = 5, 6, 7, 8, 9
 OPT_WATCHDOG_MS = 10
+OPT_CHILD_MIN = 11
 N_TH_BINS, N_E_BINS = 6, 200
 
 

@@ -136,14 +136,16 @@ enum {
      * batch is cut into launches that double the history each time, so the adaptive bias
      * counters evolve as in the serial reference (-1 = one persistent grid's worth of lanes, 0 = off) */
     GRM_OPT_WARMUP = 8,
-    /* idle lanes a wavefront gathers before it refills them together (1..64, default 2):
-     * larger = less divergent child sampling / photon set-up, more idle lane-trips */
+    /* idle lanes a wavefront gathers before it takes emitted photons (1..64, default 2) */
     GRM_OPT_REFILL_MIN = 9,
     /* per-launch watchdog in ms (default 60000, 0 = off): a transport launch running longer abandons
      * its photons and exits, and the track call fails with the reason in grm_engine_error -- no input
      * can keep the GPU busy without bound (a photon's life is bounded only by 1.28M steps x 255
      * halving attempts) */
-    GRM_OPT_WATCHDOG_MS = 10
+    GRM_OPT_WATCHDOG_MS = 10,
+    /* scattered children a wavefront samples together (1..64, default 8): larger = less divergent
+     * scattering sampling, more idle lane-trips while a batch gathers */
+    GRM_OPT_CHILD_MIN = 11
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

@@ -27,6 +27,9 @@ if os.environ.get("WARMUP"):
     e.set_option(G.OPT_WARMUP, int(os.environ["WARMUP"]))
     print(f"warmup {os.environ['WARMUP']}", flush=True)
 e.set_option(G.OPT_WATCHDOG_MS, int(os.environ.get("WATCHDOG_MS", "60000")))
+if os.environ.get("CHILD_MIN"):
+    e.set_option(G.OPT_CHILD_MIN, int(os.environ["CHILD_MIN"]))
+    print(f"child_min {os.environ['CHILD_MIN']}", flush=True)
 if os.environ.get("REFILL_MIN"):
     e.set_option(G.OPT_REFILL_MIN, int(os.environ["REFILL_MIN"]))
     print(f"refill_min {os.environ['REFILL_MIN']}", flush=True)
