@@ -129,6 +129,7 @@ struct Ctl {
     unsigned long long stuck_cap, *stuck_count;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
+constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
 
 /* Per-step (or rarer) lane fields: registers in the one-wave build; in the two-wave build
  * (GRM_LANE_LDS) an LDS column per lane ([field][lane], conflict-free), read and written where used
@@ -841,7 +842,10 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     bool warm = C.admit_n != 0;  /* wave-uniform: warm-up admission in force */
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
     L.flight = 0;
-    double bias_d = bias_den(P, C); /* wave-uniform, refreshed every 16 trips when live */
+    /* wave-uniform; refreshed every trip during the warm-up and every REFRESH_TRIPS trips after it
+     * (the device-coherent counters cost a cross-die round trip; past the warm-up they move by
+     * parts per million between refreshes) */
+    double bias_d = bias_den(P, C);
     unsigned trip = 1;
     /* per-lane launch counters, 32-bit in the loop (a lane makes < 2^32 steps per launch), widened
      * for the wave reduction at exit */
@@ -852,7 +856,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     while (true) {
         ++wave_trips;
         TCOUNT(4);
-        if ((trip++ & 15) == 0 || warm) {
+        if ((trip++ & (REFRESH_TRIPS - 1)) == 0 || warm) {
             flush_counters(C);
             if (!C.bias_frozen) bias_d = bias_den(P, C);
             if (C.watchdog_ticks) {
