@@ -55,14 +55,14 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--photon-n", type=float, default=1e6, help="photon_n per GPU")
     ap.add_argument("--grid", type=int, default=192)
     ap.add_argument("--dump", default="", help="HARM dump to use (default: synthetic dump019-class)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--threads", type=int, default=0)
-    ap.add_argument("--jobs", type=int, default=8,
+    ap.add_argument("--jobs", type=int, default=16,
                     help="run_simulation passes in flight per GPU (engines with their own streams and buffers)")
     ap.add_argument("--host-emit", action="store_true",
                     help="emit on the host, upload before timing, time transport only")

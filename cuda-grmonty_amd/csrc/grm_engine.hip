@@ -38,11 +38,11 @@ using namespace grm;
 
 namespace {
 
-/* One workgroup per CU (its LDS spectrum fills most of the CU's LDS), BLOCK / 256 waves per SIMD.
- * 512 lanes (2 waves per SIMD) fit the LDS but not the registers: the kernel holds ~460 VGPR+AGPR
- * per lane at one wave per SIMD and spills ~0.9 KB per lane at 256. */
+/* One workgroup per CU, BLOCK / 256 waves per SIMD.  512 lanes (two waves per SIMD, 256 VGPRs each)
+ * is the default: the second wave issues while the first waits on a gather or a scalar/branch slot,
+ * +20% over 256 lanes (one wave per SIMD, 256 VGPRs + AGPRs) measured on MI355X. */
 #ifndef GRM_BLOCK
-#define GRM_BLOCK 256
+#define GRM_BLOCK 512
 #endif
 #ifndef GRM_WAVES_PER_SIMD
 #define GRM_WAVES_PER_SIMD (GRM_BLOCK / 256)
@@ -129,7 +129,10 @@ struct Ctl {
     unsigned long long stuck_cap, *stuck_count;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
-constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
+#ifndef GRM_REFRESH_TRIPS
+#define GRM_REFRESH_TRIPS 64
+#endif
+constexpr unsigned REFRESH_TRIPS = GRM_REFRESH_TRIPS; /* counter flush + bias refresh + watchdog period (power of 2) */
 
 /* Per-step (or rarer) lane fields: registers in the one-wave build; in the two-wave build
  * (GRM_LANE_LDS) an LDS column per lane ([field][lane], conflict-free), read and written where used
