@@ -179,7 +179,8 @@ __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(Params P, EmitParams E
 } /* namespace */
 
 int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t n_zones, unsigned long long *d_off,
-                    hipStream_t s, grm_init_photon **out, size_t *out_cap, uint64_t *n_out, std::string &err) {
+                    hipStream_t s, unsigned long long *h_total, grm_init_photon **out, size_t *out_cap, uint64_t *n_out,
+                    std::string &err) {
     auto chk = [&](hipError_t st, const char *what) {
         if (st == hipSuccess) return true;
         err = std::string(what) + ": " + hipGetErrorString(st);
@@ -189,10 +190,11 @@ int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t 
     if (n_zones == 0) return 0;
     hipLaunchKernelGGL(zone_count_scan, dim3(1), dim3(SCAN_THREADS), 0, s, E.zones, z0, n_zones, E.k0, E.k1, d_off);
     if (!chk(hipGetLastError(), "zone_count_scan")) return -1;
-    unsigned long long total = 0;
-    if (!chk(hipMemcpyAsync(&total, d_off + n_zones, sizeof(total), hipMemcpyDeviceToHost, s), "D2H") ||
+    /* h_total: pinned host word (a DMA transfer, no blit kernel competing for CUs) */
+    if (!chk(hipMemcpyAsync(h_total, d_off + n_zones, sizeof(*h_total), hipMemcpyDeviceToHost, s), "D2H") ||
         !chk(hipStreamSynchronize(s), "sync"))
         return -1;
+    const unsigned long long total = *h_total;
     if (total > *out_cap) {
         if (*out) (void)hipFree(*out);
         *out = nullptr;

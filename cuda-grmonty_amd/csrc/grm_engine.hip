@@ -1099,7 +1099,6 @@ struct grm_engine {
     unsigned long long ovf_cap = 0;
     unsigned long long *d_small = nullptr; /* [0] pool head, [1..2] ovf counts, [3] trace count,
                                               [4] warm-up in flight, [5] warm-up admitted end */
-    unsigned long long h_small[2] = {0, 0};
     grm_init_photon *d_batch = nullptr;
     size_t batch_cap = 0;
     grm_trace *d_trace = nullptr;
@@ -1124,6 +1123,15 @@ struct grm_engine {
     int64_t watchdog_ms = 60000;           /* per-launch watchdog (GRM_OPT_WATCHDOG_MS; 0 = off) */
     double *d_stuck = nullptr;             /* [STUCK_CAP][STUCK_WORDS] abandoned-photon records */
     double *d_spec_blocks = nullptr;       /* per-workgroup spectrum slices (GRM_SPEC_LDS == 0) */
+    /* pinned host staging for the per-pass small transfers: resets are H2D copies from pin->zero and
+     * readbacks land in pin->ctr / pin->word, all on the engine stream -- DMA engine transfers, where
+     * pageable copies and hipMemset would each need a blit/fill kernel, i.e. a free CU, which with
+     * other engines' transport blocks holding every CU can take seconds to get */
+    struct Pinned {
+        unsigned long long zero[16384]; /* 128 KB >= the spectrum */
+        DevCounters ctr;
+        unsigned long long word[8];
+    } *pin = nullptr;
     /* device emission: zone table, emission tables, zone offsets, emitted photons */
     grm_emit_zone *d_ezones = nullptr;
     double *d_eweight = nullptr, *d_ef = nullptr;
@@ -1146,6 +1154,24 @@ bool hip_ok(grm_engine *e, hipError_t st, const char *what) {
     do {                                                  \
         if (!hip_ok((e), (call), #call)) return -1;       \
     } while (0)
+
+/* stream-ordered small transfers through the pinned staging block (see grm_engine::pin) */
+int zero_async(grm_engine *e, void *dev, size_t bytes) {
+    while (bytes) {
+        const size_t k = std::min(bytes, sizeof(e->pin->zero));
+        HIPCHK(e, hipMemcpyAsync(dev, e->pin->zero, k, hipMemcpyHostToDevice, e->stream));
+        dev = static_cast<char *>(dev) + k;
+        bytes -= k;
+    }
+    return 0;
+}
+
+int read_counters(grm_engine *e, DevCounters &h) {
+    HIPCHK(e, hipMemcpyAsync(&e->pin->ctr, e->d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    h = e->pin->ctr;
+    return 0;
+}
 
 int alloc_lanes(grm_engine *e) {
     int n_cu = 0;
@@ -1236,8 +1262,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
         C.f_maxtau = e->fz_maxtau;
     } else if (e->bias_mode) {
         DevCounters h;
-        HIPCHK(e, hipMemcpyAsync(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (read_counters(e, h)) return -1;
         C.f_scatt = (double)h.n_scatt;
         C.f_rec = (double)h.n_recorded;
         double mt;
@@ -1247,7 +1272,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     unsigned long long steps_before = 0;
     {
         DevCounters h;
-        HIPCHK(e, hipMemcpy(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+        if (read_counters(e, h)) return -1;
         steps_before = h.n_steps;
     }
     double ms_total = 0.0;
@@ -1255,13 +1280,13 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     int src = -1, dst = 0;
     unsigned long long n_pool = n;
     for (int pass = 0; n_pool > 0; ++pass) {
-        HIPCHK(e, hipMemsetAsync(e->d_small, 0, 3 * sizeof(unsigned long long), e->stream));
+        if (zero_async(e, e->d_small, 3 * sizeof(unsigned long long))) return -1;
         if (pass == 0 && C.admit_n) { /* [4] in flight = 0, [5] end of the first warm-up batch */
             const unsigned long long h = C.admit_h0;
-            e->h_small[0] = 0;
-            e->h_small[1] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
+            e->pin->word[2] = 0;
+            e->pin->word[3] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
                                                                         64ull, std::min(h, C.admit_lim - h)));
-            HIPCHK(e, hipMemcpyAsync(e->d_small + 4, e->h_small, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice,
+            HIPCHK(e, hipMemcpyAsync(e->d_small + 4, &e->pin->word[2], 2 * sizeof(unsigned long long), hipMemcpyHostToDevice,
                                      e->stream));
         }
         C.ovf = e->d_ovf[dst];
@@ -1272,16 +1297,16 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
             C.n_pool = n_pool;
             C.admit_n = 0;
         }
-        HIPCHK(e, hipMemsetAsync(&e->d_ctr->abort, 0, sizeof(unsigned long long), e->stream));
+        if (zero_async(e, &e->d_ctr->abort, sizeof(unsigned long long))) return -1;
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
         hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
-        unsigned long long cnt = 0;
+        HIPCHK(e, hipMemcpyAsync(&e->pin->word[0], C.ovf_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 e->stream));
         DevCounters hp;
-        HIPCHK(e, hipMemcpyAsync(&cnt, C.ovf_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipMemcpyAsync(&hp, e->d_ctr, sizeof(hp), hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (read_counters(e, hp)) return -1;
+        const unsigned long long cnt = e->pin->word[0];
         float ms = 0.f;
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
         ms_total += ms;
@@ -1308,7 +1333,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
         }
     }
     DevCounters h;
-    HIPCHK(e, hipMemcpy(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+    if (read_counters(e, h)) return -1;
     e->stats.kernel_ms += ms_total;
     e->stats.last_kernel_ms += ms_total;
     e->stats.last_steps += h.n_steps - steps_before;
@@ -1340,13 +1365,14 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
 }
 
 int reset_counters(grm_engine *e) {
-    HIPCHK(e, hipMemsetAsync(e->d_spec, 0, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS, e->stream));
-    DevCounters h;
+    if (zero_async(e, e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS)) return -1;
+    DevCounters &h = e->pin->ctr;
     std::memset(&h, 0, sizeof(h));
     std::memcpy(&h.max_tau_bits, &e->max_tau_init, sizeof(double));
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_small, 0, 4 * sizeof(unsigned long long), e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_small + 6, 0, sizeof(unsigned long long), e->stream));
+    if (zero_async(e, e->d_small, 4 * sizeof(unsigned long long)) ||
+        zero_async(e, e->d_small + 6, sizeof(unsigned long long)))
+        return -1;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return 0;
 }
@@ -1373,6 +1399,10 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     if (!hip_ok(e, hipSetDevice(device), "hipSetDevice")) return fail();
     if (!hip_ok(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking), "stream")) return fail();
     if (!hip_ok(e, hipEventCreate(&e->ev0), "event") || !hip_ok(e, hipEventCreate(&e->ev1), "event")) return fail();
+    if (!hip_ok(e, hipHostMalloc(reinterpret_cast<void **>(&e->pin), sizeof(grm_engine::Pinned), hipHostMallocDefault),
+                "pinned staging"))
+        return fail();
+    std::memset(e->pin, 0, sizeof(grm_engine::Pinned));
     const size_t nz = (size_t)h->n[0] * h->n[1];
     std::vector<double> zones(nz * 8);
     for (size_t z = 0; z < nz; ++z)
@@ -1447,6 +1477,7 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_small);
     hipFree(e->d_stuck);
     hipFree(e->d_spec_blocks);
+    if (e->pin) hipHostFree(e->pin);
     hipFree(e->d_batch);
     hipFree(e->d_trace);
     hipFree(e->d_upload);
@@ -1520,8 +1551,7 @@ int grm_engine_finish(grm_engine *e, grm_spectrum_cell *spec, uint64_t *n_rec, u
     if (spec)
         HIPCHK(e, hipMemcpyAsync(spec, e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS,
                                  hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipMemcpyAsync(&h, e->d_ctr, sizeof(h), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (read_counters(e, h)) return -1;
     if (n_rec) *n_rec = h.n_recorded;
     if (n_scatt) *n_scatt = h.n_scatt;
     if (max_tau) std::memcpy(max_tau, &h.max_tau_bits, sizeof(double));
@@ -1638,7 +1668,7 @@ int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_in
     E.k1 = (uint32_t)(seed >> 32);
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     uint64_t n = 0;
-    if (grm_emit_launch(e->P, E, (uint64_t)z0, (uint64_t)(z1 - z0), e->d_eoff, e->stream, &e->d_emit, &e->emit_cap,
+    if (grm_emit_launch(e->P, E, (uint64_t)z0, (uint64_t)(z1 - z0), e->d_eoff, e->stream, &e->pin->word[4], &e->d_emit, &e->emit_cap,
                         &n, e->err))
         return -1;
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
