@@ -88,7 +88,8 @@ struct Params {
 /* ------------------------------------------------------------------------- */
 struct Rng {
     uint32_t k0, k1;
-    uint64_t id, ctr;
+    uint64_t id;
+    uint32_t ctr, ctr_hi; /* counter words 0, 1: draw index, and the emission slot (0 in transport) */
 };
 
 __device__ __forceinline__ void philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
@@ -115,7 +116,7 @@ __device__ __forceinline__ void philox_block(uint32_t c0, uint32_t c1, uint32_t 
 /* uniform double in (0, 1] from 53 random bits */
 __device__ __forceinline__ double uniform(Rng &g) {
     uint32_t o0, o1;
-    philox_block((uint32_t)g.ctr, (uint32_t)(g.ctr >> 32), (uint32_t)g.id, (uint32_t)(g.id >> 32), g.k0, g.k1, o0,
+    philox_block(g.ctr, g.ctr_hi, (uint32_t)g.id, (uint32_t)(g.id >> 32), g.k0, g.k1, o0,
                  o1);
     ++g.ctr;
     const uint64_t m = ((((uint64_t)o1) << 32) | o0) >> 11;

@@ -43,7 +43,8 @@ __device__ __forceinline__ Rng zone_rng(uint32_t k0, uint32_t k1, uint64_t z, ui
     r.k0 = k0;
     r.k1 = k1;
     r.id = ((uint64_t)(EMIT_SALT ^ (uint32_t)(z >> 32)) << 32) | (uint32_t)z;
-    r.ctr = slot << 32;
+    r.ctr = 0;
+    r.ctr_hi = (uint32_t)slot;
     return r;
 }
 

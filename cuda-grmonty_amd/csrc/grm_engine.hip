@@ -142,11 +142,9 @@ constexpr unsigned REFRESH_TRIPS = GRM_REFRESH_TRIPS; /* counter flush + bias re
 #endif
 #define GRM_LANE_XFIELDS(X)                                                                          \
     X(tau_abs, 0) X(tau_scatt, 1) X(alpha_scatti, 2) X(alpha_absi, 3) X(bi, 4) X(fl_ne, 5)          \
-    X(ph2_x0, 6)      /* photon_2's x^0 (the rest of it is in the ph2 LDS slot) */                  \
-    X(ph2_e0s, 7)     /* photon_2's e_0_s */                                                          \
-    X(bk_x0, 8)       /* x^0 of the halving backup (the rest of it is in the bk LDS slot) */          \
-    X(p_dtau_abs, 9) X(p_dtau_scatt, 10) X(p_wc, 11) /* carried across the re-push */
-constexpr int LANE_XFIELDS = 12;
+    X(ph2_e0s, 6)     /* photon_2's e_0_s (its x^1..3, k, dk are in the ph2 LDS slot) */              \
+    X(p_dtau_abs, 7) X(p_dtau_scatt, 8) X(p_wc, 9) /* carried across the re-push */
+constexpr int LANE_XFIELDS = 10;
 
 /* hot photon state: lives in VGPRs (and, see above, LDS) for the photon's whole life */
 struct Lane {
@@ -379,6 +377,7 @@ __device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L
     L.n_scatt = 0;
     L.rng.id = C.id_base + idx;
     L.rng.ctr = 0;
+    L.rng.ctr_hi = 0;
     Cold c;
     c.e = v[4].y;
     c.l = v[5].x;
@@ -399,6 +398,7 @@ __device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L
 __device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane &L, Cold *cold) {
     L.rng.id = R.id;
     L.rng.ctr = 0;
+    L.rng.ctr_hi = 0;
     L.w = R.w;
     L.n_scatt = R.n_scatt;
 #pragma unroll
@@ -483,7 +483,9 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const 
     SReq R;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        R.x[i] = L.x[i];
+        /* x^0 (Boyer-Lindquist time) enters no result -- not the metric (stationary), the fluid, the
+         * record or any test -- so the device does not carry it: children start at x^0 = 0 */
+        R.x[i] = i == 0 ? 0.0 : L.x[i];
         R.k[i] = L.k[i];
         R.u_con[i] = F.u_con[i];
         R.b_con[i] = F.b_con[i];
@@ -544,13 +546,11 @@ __device__ __forceinline__ void load_xkdk(const Slot &s, Lane &L) {
 }
 
 __device__ __forceinline__ void store_ph2(const Slot &ph2, Lane &L) {
-    L.ph2_x0() = L.x[0];
     L.ph2_e0s() = L.e_0_s;
     save_xkdk(ph2, L);
 }
 
 __device__ __forceinline__ void load_ph2(const Slot &ph2, Lane &L) {
-    L.x[0] = L.ph2_x0();
     load_xkdk(ph2, L);
 }
 
@@ -611,7 +611,6 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     bool have_tg = false;
     if (setup || !(L.x[1] < P.xs1)) {
         if (L.depth > 0) {
-            L.bk_x0() = L.x[0];
             save_xkdk(bk, L);
         }
         double e_1;
@@ -632,7 +631,6 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             if (L.depth == 0) {
                 load_ph2(ph2, L);
             } else {
-                L.x[0] = L.bk_x0();
                 load_xkdk(bk, L);
             }
             ++L.depth;

@@ -159,7 +159,8 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
         g.k0 = (uint32_t)seed;
         g.k1 = (uint32_t)(seed >> 32);
         g.id = (uint64_t)a[1];
-        g.ctr = (uint64_t)a[2];
+        g.ctr = (uint32_t)(uint64_t)a[2];
+        g.ctr_hi = (uint32_t)((uint64_t)a[2] >> 32);
         for (int i = 0; i < 8; ++i) store(o, i, uniform(g));
         break;
     }
@@ -173,6 +174,7 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
         g.k1 = (uint32_t)(seed >> 32);
         g.id = (uint64_t)a[so + 1];
         g.ctr = 0;
+        g.ctr_hi = 0;
         if (which == 12) {
             double k[4] = {a[0], a[1], a[2], a[3]}, p[4];
             sample_electron(g, k, p, a[4]);
