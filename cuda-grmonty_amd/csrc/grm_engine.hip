@@ -145,6 +145,15 @@ constexpr unsigned REFRESH_TRIPS = GRM_REFRESH_TRIPS; /* counter flush + bias re
     X(ph2_e0s, 6)     /* photon_2's e_0_s (its x^1..3, k, dk are in the ph2 LDS slot) */              \
     X(p_dtau_abs, 7) X(p_dtau_scatt, 8) X(p_wc, 9) /* carried across the re-push */
 constexpr int LANE_XFIELDS = 10;
+#if GRM_LANE_LDS
+/* [field][lane], indexed with threadIdx.x so that every access is one ds_read/ds_write_b64 with an
+ * immediate offset (a generic pointer here would turn them into FLAT accesses, which also count in
+ * vmcnt and cost a 64-bit address register each) */
+__shared__ double s_lanex[LANE_XFIELDS * GRM_BLOCK];
+/* volatile (the compiler must not keep the fields in registers across trips -- the point is to free
+ * them) and typed in the LDS address space (a generic volatile access becomes FLAT + vmcnt waits) */
+typedef __attribute__((address_space(3))) volatile double LdsDouble;
+#endif
 
 /* hot photon state: lives in VGPRs (and, see above, LDS) for the photon's whole life */
 struct Lane {
@@ -159,9 +168,8 @@ struct Lane {
     uint32_t pend;
     double dl, hlen;                      /* step size of this iteration; length being pushed */
 #if GRM_LANE_LDS
-    volatile double *xs;                  /* this lane's LDS column */
 #define X(name, i) \
-    __device__ __forceinline__ volatile double &name() const { return xs[(i) * GRM_BLOCK]; }
+    __device__ __forceinline__ LdsDouble &name() const { return ((LdsDouble *)s_lanex)[(i) * GRM_BLOCK + threadIdx.x]; }
 #else
     double xf[LANE_XFIELDS];
 #define X(name, i)                                                           \
@@ -810,11 +818,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) < 16) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
 #endif
-#if GRM_LANE_LDS
-    __shared__ double lds[(2 * LDS_DOUBLES_PER_LANE + LANE_XFIELDS) * BLOCK];
-#else
     __shared__ double lds[2 * LDS_DOUBLES_PER_LANE * BLOCK];
-#endif
     const Slot ph2{lds + threadIdx.x, BLOCK};
     const Slot bk{lds + LDS_DOUBLES_PER_LANE * BLOCK + threadIdx.x, BLOCK};
     const unsigned lane_id = threadIdx.x & 63;
@@ -833,9 +837,6 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long wave_trips = 0;
     Lane L;
-#if GRM_LANE_LDS
-    L.xs = lds + 2 * LDS_DOUBLES_PER_LANE * BLOCK + threadIdx.x;
-#endif
     L.rng.k0 = C.key0;
     L.rng.k1 = C.key1;
     bool active = false;
