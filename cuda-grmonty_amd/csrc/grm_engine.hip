@@ -145,6 +145,12 @@ constexpr unsigned REFRESH_TRIPS = GRM_REFRESH_TRIPS; /* counter flush + bias re
     X(ph2_e0s, 6)     /* photon_2's e_0_s (its x^1..3, k, dk are in the ph2 LDS slot) */              \
     X(p_dtau_abs, 7) X(p_dtau_scatt, 8) X(p_wc, 9) /* carried across the re-push */
 constexpr int LANE_XFIELDS = 10;
+#define GRM_LANE_IFIELDS(X)                                                                          \
+    X(n_scatt, 0)                                                                                    \
+    X(flight, 1) /* warm-up: photons started (+) / ended (-) since the last flush */                \
+    /* the lane's launch counters (widened and wave-reduced at exit) */                              \
+    X(c_steps, 2) X(c_tracked, 3) X(c_primaries, 4) X(c_children, 5) X(c_nstep_max, 6) X(c_long, 7)
+constexpr int LANE_IFIELDS = 8;
 #if GRM_LANE_LDS
 /* [field][lane], indexed with threadIdx.x so that every access is one ds_read/ds_write_b64 with an
  * immediate offset (a generic pointer here would turn them into FLAT accesses, which also count in
@@ -153,14 +159,15 @@ __shared__ double s_lanex[LANE_XFIELDS * GRM_BLOCK];
 /* volatile (the compiler must not keep the fields in registers across trips -- the point is to free
  * them) and typed in the LDS address space (a generic volatile access becomes FLAT + vmcnt waits) */
 typedef __attribute__((address_space(3))) volatile double LdsDouble;
+__shared__ int s_lanei[LANE_IFIELDS * GRM_BLOCK];
+typedef __attribute__((address_space(3))) volatile int LdsInt;
 #endif
 
 /* hot photon state: lives in VGPRs (and, see above, LDS) for the photon's whole life */
 struct Lane {
     double x[4], k[4], dk[4];
     double w, e_0_s;
-    int n_scatt, n_step;
-    int flight;                           /* warm-up: photons started (+) / ended (-) since the last flush */
+    int n_step;
     Rng rng;
     /* per-trip push state machine: phase 0 = loop top, 1 = geodesic step in progress,
      * 2 = re-push to the scattering point in progress; depth/pend = position in the halving tree */
@@ -170,14 +177,22 @@ struct Lane {
 #if GRM_LANE_LDS
 #define X(name, i) \
     __device__ __forceinline__ LdsDouble &name() const { return ((LdsDouble *)s_lanex)[(i) * GRM_BLOCK + threadIdx.x]; }
+#define XI(name, i) \
+    __device__ __forceinline__ LdsInt &name() const { return ((LdsInt *)s_lanei)[(i) * GRM_BLOCK + threadIdx.x]; }
 #else
     double xf[LANE_XFIELDS];
+    int xif[LANE_IFIELDS];
 #define X(name, i)                                                           \
     __device__ __forceinline__ double &name() { return xf[i]; }              \
     __device__ __forceinline__ double name() const { return xf[i]; }
+#define XI(name, i)                                                          \
+    __device__ __forceinline__ int &name() { return xif[i]; }                \
+    __device__ __forceinline__ int name() const { return xif[i]; }
 #endif
     GRM_LANE_XFIELDS(X)
+    GRM_LANE_IFIELDS(XI)
 #undef X
+#undef XI
 };
 
 /* Denominator of bias_func's first term, bias_norm * max_tau_scatt * (<N_scatt> + 2)
@@ -284,7 +299,7 @@ __device__ void write_trace(const Ctl &C, const Cold *cold, uint64_t id, double 
 
 __device__ __forceinline__ void trace_end(const Ctl &C, const Cold *cold, const Lane &L, int reason) {
     if (C.trace)
-        write_trace(C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt, L.n_step,
+        write_trace(C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt(), L.n_step,
                     reason, -1, -1);
 }
 
@@ -368,7 +383,7 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
 __device__ __forceinline__ void end_of_life(const Params &P, const Ctl &C, const Cold *cold, const Lane &L) {
     /* record_criterion (harm_model.cpp:1618) && n_step <= max_n_step (:1066) */
     if (L.x[1] > P.x1_max && L.n_step <= MAX_N_STEP)
-        record_photon(P, C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt, L.n_step);
+        record_photon(P, C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt(), L.n_step);
     else
         trace_end(C, cold, L, 2);
 }
@@ -382,7 +397,7 @@ __device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L
     L.x[0] = v[0].x; L.x[1] = v[0].y; L.x[2] = v[1].x; L.x[3] = v[1].y;
     L.k[0] = v[2].x; L.k[1] = v[2].y; L.k[2] = v[3].x; L.k[3] = v[3].y;
     L.w = v[4].x;
-    L.n_scatt = 0;
+    L.n_scatt() = 0;
     L.rng.id = C.id_base + idx;
     L.rng.ctr = 0;
     L.rng.ctr_hi = 0;
@@ -408,7 +423,7 @@ __device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane 
     L.rng.ctr = 0;
     L.rng.ctr_hi = 0;
     L.w = R.w;
-    L.n_scatt = R.n_scatt;
+    L.n_scatt() = R.n_scatt;
 #pragma unroll
     for (int i = 0; i < 4; ++i) L.x[i] = R.x[i];
     Cold c;
@@ -506,7 +521,7 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const 
     R.e_0 = cold->e_0;
     R.id = child_id(L.rng.id, L.rng.ctr);
     R.parent = L.rng.id;
-    R.n_scatt = L.n_scatt + 1;
+    R.n_scatt = L.n_scatt() + 1;
     R.pad0 = 0;
     R.pad1 = 0.0;
     const int slot = atomicAdd(wtop, 1); /* LDS; values past the cap are clamped at the next refill */
@@ -592,7 +607,7 @@ __device__ bool init_photon(const Ctl &C, const Cold *cold, Lane &L, const Slot 
  * :1279-1285) spends extra trips while the other lanes of the wave keep stepping, instead of the
  * whole wave waiting for the deepest halving tree.  Returns false when the photon's life ended. */
 __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *wstack, int *wtop,
-                               unsigned &steps, unsigned &children, const Slot &ph2,
+                               const Slot &ph2,
                                const Slot &bk, double bias_d) {
     if (L.phase == 0) {
         if (stop_criterion(P, L)) {
@@ -659,7 +674,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
      * ONE evaluation here so a wave with lanes in both phases runs that code once. */
     const bool at_scatter = L.phase == 2;
     if (!at_scatter && !setup) {
-        ++steps;
+        ++L.c_steps();
         if (stop_criterion(P, L)) {
             end_of_life(P, C, cold, L);
             return false;
@@ -720,8 +735,8 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             /* the child leaves as a scatter request; its stores go out after this trip's table
              * loads, so no load of the trip waits behind them (vmcnt is in order) */
             if (F.n_e > 0.0) {
-                if (push_request(C, L, cold, F, L.p_wc(), wstack, wtop)) ++L.flight;
-                ++children;
+                if (push_request(C, L, cold, F, L.p_wc(), wstack, wtop)) ++L.flight();
+                ++L.c_children();
             }
             L.alpha_scatti() = a_s;
             L.alpha_absi() = a_a;
@@ -843,7 +858,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     bool pool_done = false;      /* wave-uniform */
     bool warm = C.admit_n != 0;  /* wave-uniform: warm-up admission in force */
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
-    L.flight = 0;
+    L.flight() = 0;
     /* wave-uniform; refreshed every trip during the warm-up and every REFRESH_TRIPS trips after it
      * (the device-coherent counters cost a cross-die round trip; past the warm-up they move by
      * parts per million between refreshes) */
@@ -851,8 +866,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     unsigned trip = 1;
     /* per-lane launch counters, 32-bit in the loop (a lane makes < 2^32 steps per launch), widened
      * for the wave reduction at exit */
-    unsigned steps = 0, tracked = 0, primaries = 0, children = 0;
-    unsigned nstep_max = 0, n_long = 0; /* longest photon life; lives > 100k steps */
+    L.c_steps() = L.c_tracked() = L.c_primaries() = L.c_children() = 0;
+    L.c_nstep_max() = L.c_long() = 0; /* longest photon life; lives > 100k steps */
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
 
     while (true) {
@@ -974,7 +989,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                     if (idx < C.n_pool) {
                         if (C.pool_kind == 0) {
                             load_primary(C, idx, L, cold);
-                            ++primaries;
+                            ++L.c_primaries();
                         } else {
                             SReq R;
                             load_sreq(reinterpret_cast<const SReq *>(C.pool) + idx, R);
@@ -987,20 +1002,20 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                     }
                 }
                 if (has) {
-                    ++tracked;
+                    ++L.c_tracked();
                     if (ok) active = init_photon(C, cold, L, ph2);
-                    if (!active) --L.flight; /* started and ended at once (invalid) */
+                    if (!active) --L.flight(); /* started and ended at once (invalid) */
                 }
                 TSTAMP(1);
             }
         }
         if (!__any(active)) {
             if (warm) {
-                int d = L.flight; /* flush before waiting: the barrier needs everyone's ends */
+                int d = L.flight(); /* flush before waiting: the barrier needs everyone's ends */
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
                 if (lane_id == 0 && d) atomicAdd(C.in_flight, (unsigned long long)(long long)d);
-                L.flight = 0;
+                L.flight() = 0;
             }
             if (pool_done && *wtop == 0) break;
             if (warm) {
@@ -1014,19 +1029,19 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         }
         wait_trips = 0;
         if (active) {
-            active = transport_trip(P, C, L, cold, wstack, wtop, steps, children, ph2, bk, bias_d);
+            active = transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d);
             if (!active) {
-                nstep_max = max(nstep_max, (unsigned)L.n_step);
-                n_long += L.n_step > 100000 ? 1 : 0;
-                --L.flight;
+                L.c_nstep_max() = max((int)L.c_nstep_max(), L.n_step);
+                L.c_long() += L.n_step > 100000 ? 1 : 0;
+                --L.flight();
             }
         }
         if (warm) {
-            int d = L.flight;
+            int d = L.flight();
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
             if (lane_id == 0 && d) atomicAdd(C.in_flight, (unsigned long long)(long long)d);
-            L.flight = 0;
+            L.flight() = 0;
         }
         TSTAMP(2);
     }
@@ -1051,8 +1066,9 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         if (v != 0.0) unsafeAtomicAdd(reinterpret_cast<double *>(C.spec + i / SPEC_FIELDS) + i % SPEC_FIELDS, v);
     }
     /* wave-reduce the lane counters, one atomic per wave */
-    unsigned long long w_steps = steps, w_tracked = tracked, w_primaries = primaries, w_children = children;
-    unsigned long long w_long = n_long, w_nstep_max = nstep_max;
+    unsigned long long w_steps = (unsigned)L.c_steps(), w_tracked = (unsigned)L.c_tracked();
+    unsigned long long w_primaries = (unsigned)L.c_primaries(), w_children = (unsigned)L.c_children();
+    unsigned long long w_long = (unsigned)L.c_long(), w_nstep_max = (unsigned)L.c_nstep_max();
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         w_steps += __shfl_xor(w_steps, off);
@@ -1073,7 +1089,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         wr[0] = rt_start;
         wr[1] = __builtin_amdgcn_s_memrealtime();
         wr[2] = wave_trips;
-        wr[3] = tracked;
+        wr[3] = w_tracked;
     }
 }
 
