@@ -159,11 +159,19 @@ struct Trig {
     double sth, cth; /* sin/cos(theta_BL) */
 };
 
+/* theta = pi x2 + (1 - h)/2 sin(2 pi x2) (harm_model.cpp gcov/connection): both sincos through
+ * sincospi of x2-scaled arguments -- an exact, branch-free range reduction instead of the general
+ * one (agreement with sin/cos of the pi-multiplied argument to a few ulp) */
 __device__ __forceinline__ void trig_at(const Params &P, const double x[4], Trig &T) {
     T.r1 = exp(x[1]);
+#ifndef GRM_TRIG_GENERAL
+    sincospi(2.0 * x[2], &T.s2x, &T.c2x);
+    sincospi(x[2] + ((1.0 - P.h_slope) / (2.0 * kPi)) * T.s2x, &T.sth, &T.cth);
+#else
     sincos(2.0 * kPi * x[2], &T.s2x, &T.c2x);
     const double th = kPi * x[2] + ((1.0 - P.h_slope) / 2.0) * T.s2x;
     sincos(th, &T.sth, &T.cth);
+#endif
 }
 
 /* non-zero g_mu,nu of MKS Kerr + g^{00}, g^{01} (g^{02} = g^{03} = 0) */
