@@ -431,7 +431,11 @@ struct Fluid {
 /* cell-centred zone index and bilinear weights of x (x_to_ij, harm_model.cpp:1406-1434, with the
  * edge clamp of interp_scalar); false = out of the grid */
 __device__ __forceinline__ bool zone_index(const Params &P, const double x[4], int &i, int &j, double &di, double &dj) {
-    if (x[1] < P.xs1 || x[1] > P.xe1 || x[2] < P.xs2 || x[2] > P.xe2) return false;
+    if (x[1] < P.xs1 || x[1] > P.xe1 || x[2] < P.xs2 || x[2] > P.xe2) {
+        i = j = 0; /* a valid zone, so callers may load unconditionally and select afterwards */
+        di = dj = 0.0;
+        return false;
+    }
     const double t1 = fdiv(x[1] - P.xs1, P.dx1), t2 = fdiv(x[2] - P.xs2, P.dx2);
     i = (int)(t1 - 0.5 + 1000) - 1000;
     j = (int)(t2 - 0.5 + 1000) - 1000;
@@ -465,7 +469,7 @@ struct ZoneFetch {
 __device__ __forceinline__ void zone_fetch(const Params &P, const double x[4], ZoneFetch &Z) {
     int i, j;
     double di, dj;
-    if (!zone_index(P, x, i, j, di, dj)) return;
+    zone_index(P, x, i, j, di, dj); /* out of the grid: zone (0, 0), result unused */
     const double2 *z0 = reinterpret_cast<const double2 *>(P.zones + ((size_t)i * P.n2 + j) * 8);
     const double2 *z1 = reinterpret_cast<const double2 *>(P.zones + ((size_t)(i + 1) * P.n2 + j) * 8);
 #pragma unroll
@@ -480,13 +484,7 @@ __device__ __forceinline__ void fluid_from(const Params &P, const double x[4], c
                                            Fluid &F) {
     int i, j;
     double di, dj;
-    if (!zone_index(P, x, i, j, di, dj)) {
-        /* out of grid: n_e = 0; the reference leaves the rest unset, we zero it (so does the oracle) */
-        F.n_e = F.theta_e = F.b = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) F.u_con[q] = F.u_cov[q] = F.b_con[q] = F.b_cov[q] = 0.0;
-        return;
-    }
+    const bool in_grid = zone_index(P, x, i, j, di, dj);
     const double c0 = (1.0 - di) * (1.0 - dj), c1 = (1.0 - di) * dj, c2 = di * (1.0 - dj), c3 = di * dj;
     double v[8];
 #pragma unroll
@@ -516,6 +514,13 @@ __device__ __forceinline__ void fluid_from(const Params &P, const double x[4], c
     lower(G, F.b_con, F.b_cov);
     F.b = sqrt(F.b_con[0] * F.b_cov[0] + F.b_con[1] * F.b_cov[1] + F.b_con[2] * F.b_cov[2] + F.b_con[3] * F.b_cov[3]) *
           P.b_unit;
+    if (!in_grid) {
+        /* out of grid: n_e = 0; the reference leaves the rest unset, we zero it (so does the oracle).
+         * Computed on zone (0, 0) and discarded, branch-free (no per-lane stack copies) */
+        F.n_e = F.theta_e = F.b = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F.u_con[q] = F.u_cov[q] = F.b_con[q] = F.b_cov[q] = 0.0;
+    }
 }
 
 __device__ __forceinline__ void fluid_params(const Params &P, const double x[4], const Gcov &G, Fluid &F) {
