@@ -67,6 +67,14 @@ __device__ __forceinline__ double frcp(double b) { return 1.0 / b; }
 __device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
 __device__ __forceinline__ double fratio_tol(double a, double b) { return fabs(a / b); }
 #endif
+/* a / b for a kernel-argument divisor b with host reciprocal ib: one multiply (<= 1 ulp from a / b;
+ * only grid / table coordinates go through it, whose interpolants are continuous across cells).
+ * -DGRM_DIV_PARAMS restores the division (A/B builds). */
+#ifndef GRM_DIV_PARAMS
+__device__ __forceinline__ double udiv(double a, double, double ib) { return a * ib; }
+#else
+__device__ __forceinline__ double udiv(double a, double b, double) { return fdiv(a, b); }
+#endif
 
 /* Kernel-argument block: everything uniform across lanes (lands in SGPRs). */
 struct Params {
@@ -78,6 +86,7 @@ struct Params {
     double hc_l_min_w, hc_l_min_t, hc_d_l_w, hc_d_l_t;
     double jnu_l_min_t, jnu_d_l_t;
     double spec_l_e_0, th_dx2;
+    double i_dx1, i_dx2, hc_i_d_l_w, hc_i_d_l_t, jnu_i_d_l_t; /* host reciprocals of the uniform divisors */
     const double *zones;    /* [n1*n2][8]: rho,u,u1,u2,u3,B1,B2,B3 (64 B per zone) */
     const double *hotcross; /* [221][81] log10 sigma */
     const double *k2;       /* [201] log K2 */
@@ -243,7 +252,12 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
     const double fac2 = a2 + 2.0 * r2 + a2 * c2th;
     const double fac3 = a2 + r1 * (-2.0 + r1);
     const double i_r1rho23 = frcp(r1) * irho23;
+#ifdef GRM_FAC2_RCP
     const double i_sth = frcp(sth), ifac2 = frcp(fac2);
+#else
+    /* fac2 = a^2 + 2 r^2 + a^2 cos(2 theta) = 2 rho^2: one reciprocal fewer (agreement to an ulp) */
+    const double i_sth = frcp(sth), ifac2 = 0.5 * irho2;
+#endif
 
     C.c[0][0] = 2.0 * r1 * fac1_rho23;
     C.c[0][1] = r1 * (2.0 * r1 + rho2) * fac1_rho23;
@@ -316,6 +330,7 @@ __device__ __forceinline__ void init_dkdlam(const Params &P, const double x[4], 
 
 /* harm_model.cpp:1620-1630 */
 __device__ __forceinline__ double step_size(const Params &P, const double x[4], const double k[4]) {
+#ifdef GRM_STEP_SEVEN_DIV
     const double dl_x_1 = fdiv(STEP_EPS * x[1], fabs(k[1]) + EPS);
     const double dl_x_2 = fdiv(STEP_EPS * fmin(x[2], P.xe2 - x[2]), fabs(k[2]) + EPS);
     const double dl_x_3 = fdiv(STEP_EPS, fabs(k[3]) + EPS);
@@ -323,6 +338,15 @@ __device__ __forceinline__ double step_size(const Params &P, const double x[4], 
     const double i2 = frcp(fabs(dl_x_2) + EPS);
     const double i3 = frcp(fabs(dl_x_3) + EPS);
     return frcp(i1 + i2 + i3);
+#else
+    /* 1 / (|a / b| + EPS) = b / (|a| + EPS b) with b = |k| + EPS > 0: four divisions instead of
+     * seven (same value to rounding; a = 0 still gives 1 / EPS) */
+    const double b1 = fabs(k[1]) + EPS, b2 = fabs(k[2]) + EPS, b3 = fabs(k[3]) + EPS;
+    const double i1 = fdiv(b1, fabs(STEP_EPS * x[1]) + EPS * b1);
+    const double i2 = fdiv(b2, fabs(STEP_EPS * fmin(x[2], P.xe2 - x[2])) + EPS * b2);
+    const double i3 = fdiv(b3, STEP_EPS + EPS * b3);
+    return frcp(i1 + i2 + i3);
+#endif
 }
 
 /* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
@@ -436,7 +460,7 @@ __device__ __forceinline__ bool zone_index(const Params &P, const double x[4], i
         di = dj = 0.0;
         return false;
     }
-    const double t1 = fdiv(x[1] - P.xs1, P.dx1), t2 = fdiv(x[2] - P.xs2, P.dx2);
+    const double t1 = udiv(x[1] - P.xs1, P.dx1, P.i_dx1), t2 = udiv(x[2] - P.xs2, P.dx2, P.i_dx2);
     i = (int)(t1 - 0.5 + 1000) - 1000;
     j = (int)(t2 - 0.5 + 1000) - 1000;
     if (i < 0) {
@@ -694,13 +718,13 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
     const bool hc_table = !hc_thomson && !hc_kn && !hc_num;
     double fi = 0.0, fj = 0.0;
     if (hc_table) {
-        fi = fdiv(log10(w) - P.hc_l_min_w, P.hc_d_l_w);
-        fj = fdiv(ln_te * kLog10E - P.hc_l_min_t, P.hc_d_l_t);
+        fi = udiv(log10(w) - P.hc_l_min_w, P.hc_d_l_w, P.hc_i_d_l_w);
+        fj = udiv(ln_te * kLog10E - P.hc_l_min_t, P.hc_d_l_t, P.hc_i_d_l_t);
     }
     const int i = hc_table ? (int)fi : 0, j = hc_table ? (int)fj : 0;
     /* K2 index (jnu_mixed.cpp:102-111, 150-158) */
     const bool k2_table = !(theta_e < THETA_E_MIN) && !(theta_e > JNU_MAX_T);
-    double dk = k2_table ? fdiv(ln_te - P.jnu_l_min_t, P.jnu_d_l_t) : 0.0;
+    double dk = k2_table ? udiv(ln_te - P.jnu_l_min_t, P.jnu_d_l_t, P.jnu_i_d_l_t) : 0.0;
     const int ik = k2_table ? min((int)dk, GRM_N_E_SAMP - 1) : 0;
     const double *t = P.hotcross + (size_t)i * (HC_N_T + 1) + j;
     const double t00 = t[0], t01 = t[1], t10 = t[HC_N_T + 1], t11 = t[HC_N_T + 2];

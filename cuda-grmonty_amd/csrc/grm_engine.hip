@@ -1465,6 +1465,11 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     P.jnu_d_l_t = std::log(1.0e2 / 0.3) / GRM_N_E_SAMP;
     P.spec_l_e_0 = std::log(1.0e-12);
     P.th_dx2 = (h->x_stop[2] - h->x_start[2]) / (2.0 * N_TH_BINS);
+    P.i_dx1 = 1.0 / P.dx1;
+    P.i_dx2 = 1.0 / P.dx2;
+    P.hc_i_d_l_w = 1.0 / P.hc_d_l_w;
+    P.hc_i_d_l_t = 1.0 / P.hc_d_l_t;
+    P.jnu_i_d_l_t = 1.0 / P.jnu_d_l_t;
     P.zones = e->d_zones;
     P.hotcross = e->d_hot;
     P.k2 = e->d_k2;
