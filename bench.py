@@ -1,37 +1,42 @@
 """bench.py -- superphotons/s of the MI355X transport engine on the dump019-class config.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--photon-n 1e6] [--grid 192]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--photon-n 1e6] [--grid 192] [--scaling weak|strong]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Workload (BASELINE.json configs[1]): dump019 at photon_n = 1e6, mass_unit = 4e19.  dump019 is not
 available offline, so a deterministic synthetic HARM dump of dump019's class (192x192 MKS torus,
 a = 0.9375; cuda-grmonty_amd/grmonty_amd/synth_dump.py) is used -- "data": "synthetic".
-A step = one run_simulation pass (harm_model.cpp:340-414) on the GPU: the superphotons are emitted on
-the device from the zone table already resident in HBM (grm_engine_emit: zone counts, scan,
-sample_zone_photon), every one of them is tracked to completion (scattered children included), then
-spectrum + counters are reduced.  `--host-emit` instead times transport only, over photons emitted
-on the host and uploaded before the timed region (the previous definition of a step).
 
-Passes in flight (--jobs, default 4): each pass runs on its own engine (stream, buffers, spectrum,
-counters, bias state) from its own host thread.  A pass ends with a few long-lived superphotons
-(polar Zeno-stepping or full-depth step halving, up to ~1e6 serial push attempts, one lane on one
-CU); the next passes' photons fill the other CUs meanwhile.  Every pass is complete; value is the
-sustained rate of back-to-back passes, and detail.single_pass_rate / pass_latency_s report one pass
-alone.
+A step = ONE complete run_simulation pass (harm_model.cpp:340-414), run alone on the GPU: the
+superphotons are emitted on the device from the zone table already resident in HBM (grm_engine_emit:
+zone counts, scan, sample_zone_photon), every one of them is tracked to completion (scattered
+children included), spectrum + counters are reduced (RCCL all-reduce across ranks) and read back.
+Pass s of the timed region runs seed 123 + s for emission and transport (pass 0 is the reference's
+own seed, consts.hpp:14); warm-up passes use other seeds, so every pass is an independent Monte Carlo
+run.  value = superphotons created by all ranks in the K passes / max-over-ranks wall time of the K
+passes -- the reference's "Final rate" (created / elapsed of run_simulation, harm_model.cpp:407-409)
+averaged over K runs.
 
-Multi-GPU (weak scaling): N ranks run ONE job of photon_n x N whose zones are split into N
-contiguous ranges of equal expected photon count; zone emission streams and photon stream ids are
-global, so the union of the shards is exactly the single-GPU job's photon list.  The only exchange
-is the RCCL all-reduce (xGMI) of the 6x200x13 fp64 spectrum + counters, issued by the engine's C
-library on its own HIP stream.  torch.distributed is used with the gloo backend only (rendezvous,
-RCCL unique-id broadcast, barriers, max-over-ranks timing): torch's bundled HIP runtime is never
-initialised, because a second HIP runtime in the process cannot open the GPU.  Every engine call
-returns after its stream has synchronised, so the barriers bracket finished device work.
+detail.overlapped (1 GPU only, --overlap J, default 16): J such passes in flight at once (J engines,
+own streams and buffers, distinct seeds) -- device throughput when independent runs share the GPU;
+it is NOT value.
 
-value = superphotons emitted by all ranks (the reference's "created", harm_model.cpp:407-409) per
-second of max-over-ranks wall time of the K timed steps -- the reference's "Final rate" window
-(emission + transport, tables already built).
+Multi-GPU: one process per GPU.  --scaling weak (default): the job is photon_n x N, zone-sharded
+into N contiguous ranges of equal expected photon count; --scaling strong: the job is photon_n,
+zone-sharded the same way.  Zone emission streams and photon ids are global, so the union of the
+shards is exactly the single-GPU job's photon list.  The only exchange is the end-of-pass RCCL
+all-reduce (xGMI) of the 6x200x13 fp64 spectrum + counters, one communicator per rank, issued by the
+engine's C library on its stream.  torch.distributed runs with the gloo backend only (rendezvous,
+RCCL unique-id broadcast, barriers, max-over-ranks timing): torch's own HIP runtime is never
+initialised, since a second HIP runtime in the process cannot open the GPU.
+
+roofline: the dominant kernel is track_kernel; it is fp64-VALU bound.  achieved =
+exact FP64 flops per transport step (counted on the oracle restatement by an instrumented build,
+tests/golden/fp64_ops_per_step.json, tools/count_fp64.py) x transport steps of each pass's dominant
+track_kernel launch / that launch's duration (HIP events on the engine stream; passes run alone, so
+the launch is not overlapped), against the MI355X FP64 vector peak.  The HBM view (304 algorithmic
+bytes per step) is reported beside it.
 """
 from __future__ import annotations
 
@@ -48,24 +53,29 @@ sys.path.insert(0, os.path.join(REPO, "cuda-grmonty_amd"))
 import grmonty_amd as G  # noqa: E402  (load the engine's HIP runtime before anything else)
 from grmonty_amd.synth_dump import ensure_dump  # noqa: E402
 
-ALG_BYTES_PER_STEP = 304  # per transport step: HARM gather 8x4x8 + hotcross 4x8 + K2 2x8 (DESIGN.md)
+ALG_BYTES_PER_STEP = 304  # per transport step: HARM gather 8x4x8 + hotcross 4x8 + K2 2x8 (SURVEY §8d)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFS = 78.6      # MI355X FP64 vector peak (spec: 256 CU x 4 SIMD x 16 lanes x FMA x 2.4 GHz)
+FP64_COUNT = os.path.join(REPO, "tests", "golden", "fp64_ops_per_step.json")
+SEED0 = 123               # consts.hpp:14
+WARM_SEED0 = 1_000_000    # warm-up passes: seeds disjoint from the timed ones
+OVERLAP_SEED0 = 2_000_000
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--photon-n", type=float, default=1e6, help="photon_n per GPU")
+    ap.add_argument("--photon-n", type=float, default=1e6,
+                    help="photon_n per GPU (--scaling weak) or of the whole job (--scaling strong)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--grid", type=int, default=192)
     ap.add_argument("--dump", default="", help="HARM dump to use (default: synthetic dump019-class)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--threads", type=int, default=0)
-    ap.add_argument("--jobs", type=int, default=16,
-                    help="run_simulation passes in flight per GPU (engines with their own streams and buffers)")
-    ap.add_argument("--host-emit", action="store_true",
-                    help="emit on the host, upload before timing, time transport only")
+    ap.add_argument("--overlap", type=int, default=16,
+                    help="detail only: passes in flight for the overlapped-throughput figure (0 = skip; 1 GPU)")
     ap.add_argument("--pmc-summary", default=os.environ.get("GRM_PMC_SUMMARY", ""),
                     help="rocprofv3 --pmc counter CSVs, comma-separated (FETCH_SIZE pass, WRITE_SIZE pass) "
                          "of this same command, to fill roofline.traffic")
@@ -77,6 +87,15 @@ def host_threads(world: int) -> int:
     if n <= 0:
         n = min(16, os.cpu_count() or 1)
     return max(1, n // world) if world > 1 else n
+
+
+def fp64_count():
+    """exact FP64 operation counts per transport step of the oracle restatement (tools/count_fp64.py)"""
+    try:
+        with open(FP64_COUNT) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(path: str, photon_n: int, photons: np.ndarray, seconds: float):
@@ -106,13 +125,13 @@ def cpu_baseline(path: str, photon_n: int, photons: np.ndarray, seconds: float):
     t_emit = time.time() - t0
     per = t_track / max(done, 1) + t_emit / max(n_em, 1)
     return {"value": 1.0 / per, "unit": "superphotons/s", "cores": 1, "kind": "port",
-            "sample": f"{done} of the {len(photons)} emitted superphotons (random subset) tracked in {t_track:.1f} s "
+            "sample": f"{done} of the {len(photons)} superphotons of pass 0 (random subset) tracked in {t_track:.1f} s "
                       f"+ {n_em} superphotons emitted from random zones in {t_emit:.1f} s by the oracle "
                       f"(oracle/grmonty_oracle.cpp: serial reference CPU semantics, mt19937, live bias) on 1 "
-                      f"host core"}
+                      f"host core; the reference's own CPU build is not buildable here (DESIGN.md §3)"}
 
 
-def pmc_traffic(path: str, k: int):
+def pmc_traffic(path: str):
     """HBM bytes per dominant track_kernel dispatch from rocprofv3 --pmc counter CSVs (FETCH_SIZE and
     WRITE_SIZE in KB, from separate passes; gfx950 FETCH_SIZE reports half of wide streaming reads ->
     doubled, MI355X_MICROARCH.md §HBM).  `path` = comma-separated CSVs; mean over the dominant
@@ -132,29 +151,29 @@ def pmc_traffic(path: str, k: int):
                     per[c][d] = per[c].get(d, 0.0) + float(row.get("Counter_Value", 0))
     if not per["FETCH_SIZE"] or not per["WRITE_SIZE"]:
         return None
-    # the dominant launches of the profiled run (the warm-up launches are a thousand times smaller)
-    ids = [d for d in per["FETCH_SIZE"] if d in per["WRITE_SIZE"]]
-    tot = {d: 2.0 * per["FETCH_SIZE"][d] + per["WRITE_SIZE"][d] for d in ids}
-    big = [v for v in tot.values() if v >= 0.1 * max(tot.values())]
-    return float(np.mean(big)) * 1024.0
+    fetch = [v for v in per["FETCH_SIZE"].values()]
+    write = [v for v in per["WRITE_SIZE"].values()]
+    fb = [v for v in fetch if v >= 0.1 * max(fetch)]
+    wb = [v for v in write if v >= 0.1 * max(write)]
+    return (2.0 * float(np.mean(fb)) + float(np.mean(wb))) * 1024.0
 
 
 def main():
     args = parse()
-    # one hardware queue per engine (+1): a pass's long-lived last photons keep its kernel running on
-    # a CU or two, and a kernel queued behind it on a shared hardware queue would wait for it.  HIP
-    # reads this when its runtime starts (the first engine call below); 4 is the box default.
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(4, args.jobs + 1)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    overlap = args.overlap if world == 1 else 0
+    if overlap > 1:
+        # one hardware queue per engine of the overlapped figure (+1); HIP reads it at runtime start
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(4, overlap + 1)))
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
         dist.init_process_group("gloo")
     threads = args.threads or host_threads(world)
-    photon_n_job = int(args.photon_n) * world
+    photon_n_job = int(args.photon_n) * (world if args.scaling == "weak" else 1)
     path = args.dump or os.path.join(REPO, "gpurun_out" if os.path.isdir(os.path.join(REPO, "gpurun_out")) else ".",
                                      f"synth{args.grid}_r{rank}.dump")
     if not args.dump:
@@ -164,133 +183,85 @@ def main():
     t_init = time.time() - t
     shards = G.shard_zones(model.zone_weights(), world)
     z0, z1 = shards[rank]
-    counts = [model.count(seed=123, z0=a, z1=b, threads=threads) for a, b in shards]
+    timed_seeds = [SEED0 + s for s in range(args.steps)]
+    warm_seeds = [WARM_SEED0 + s for s in range(args.warmup)]
+    # per-seed photon counts of every shard (host, outside the timing): the rank's id base
     t = time.time()
-    photons = model.emit(seed=123, z0=z0, z1=z1, threads=threads)
-    t_emit = time.time() - t
-    n = len(photons)
-    assert n == counts[rank]
-    id_base = int(sum(counts[:rank]))
-    # HBM per engine: the emitted batch (128 B per superphoton) + two overflow pools (2 x n/4 x 208 B)
-    # + lane stacks; keep the engines of one GPU within ~200 GB of its 288 GB
-    per_engine = n * (128 + 104) + 0.5e9
-    jobs = max(1, min(args.jobs, int(200e9 // per_engine)))
-    engines = [G.Engine(model, device=local) for _ in range(jobs)]
-    for engine in engines:
-        engine.set_option(G.OPT_SEED, 123)
-    if world > 1:  # one RCCL communicator per concurrent pass; pass s uses engine s % jobs on every rank
-        uid = [[G.rccl_unique_id() for _ in range(jobs)] if rank == 0 else None]
+    id_base = {}
+    for sd in warm_seeds + timed_seeds:
+        id_base[sd] = sum(model.count(seed=sd, z0=a, z1=b, threads=threads) for a, b in shards[:rank])
+    t_count = time.time() - t
+    engine = G.Engine(model, device=local)
+    if world > 1:  # one RCCL communicator per rank
+        uid = [G.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        for engine, u in zip(engines, uid[0]):
-            engine.comm_init(u, world, rank)
-    # inputs resident in HBM before the timed region: the zone table (device emission) or the
-    # host-emitted photons (--host-emit)
-    for engine in engines:
-        engine.emit_setup(model)
-    d_ph = [engine.upload(photons) for engine in engines] if args.host_emit else None
+        engine.comm_init(uid[0], world, rank)
+    engine.emit_setup(model)  # the zone table is resident in HBM before the timed region
 
-    import threading
-    ar_turn = [0]
-    ar_cv = threading.Condition()
-    AR_ABORT = 1 << 60
+    def one_pass(eng, seed, base, allreduce):
+        """one run_simulation pass: emission + transport + reduction + readback"""
+        eng.reset()
+        eng.set_option(G.OPT_SEED, seed)
+        eng.set_option(G.OPT_ID_BASE, base)
+        ptr, n_dev = eng.emit(seed=seed, z0=z0, z1=z1)
+        eng.track_device(ptr, n_dev)
+        st = eng.stats()
+        if allreduce:
+            eng.allreduce()
+        spec, n_rec, n_scatt, max_tau = eng.finish()
+        if st["n_dropped"] or st["n_abandoned"]:
+            raise RuntimeError(f"pass seed {seed}: {st['n_dropped']} children dropped, {st['n_abandoned']} abandoned")
+        return n_dev, st, n_rec, n_scatt
 
-    def allreduce_in_order(engine, s_):
-        """every rank issues pass s_'s collective after passes < s_ (one global order for RCCL)"""
-        with ar_cv:
-            ar_cv.wait_for(lambda: ar_turn[0] == s_ or ar_turn[0] >= AR_ABORT)
-            if ar_turn[0] >= AR_ABORT:
-                raise RuntimeError("another pass failed")
-        try:
-            engine.allreduce()
-        finally:
-            with ar_cv:
-                ar_turn[0] += 1
-                ar_cv.notify_all()
-
-    def step(j, s_):
-        """one run_simulation pass on engine j (its own stream, buffers, spectrum and counters)"""
-        engine = engines[j]
-        t = time.time()
-        engine.reset()
-        engine.set_option(G.OPT_ID_BASE, id_base)
-        if args.host_emit:
-            engine.track_device(d_ph[j], n)
-        else:
-            ptr, n_dev = engine.emit(seed=123, z0=z0, z1=z1)
-            if n_dev != n:
-                raise RuntimeError(f"device emission made {n_dev} superphotons, host count {n}")
-            engine.track_device(ptr, n_dev)
-        st = engine.stats()
-        if world > 1:
-            allreduce_in_order(engine, s_)
-        spec, n_rec, n_scatt, max_tau = engine.finish()
-        return st, n_rec, n_scatt, time.time() - t
-
-    def run(n_steps):
-        """n_steps passes, pass s on engine s % jobs; the engines' host threads run concurrently, so a
-        pass's last long-lived superphoton (one lane on one CU) overlaps the next passes' work"""
-        res = [None] * n_steps
-        err = []
-        ar_turn[0] = 0
-
-        def worker(j):
-            try:
-                for s_ in range(j, n_steps, jobs):
-                    res[s_] = step(j, s_)
-            except Exception as ex:  # surfaced below
-                err.append(ex)
-                with ar_cv:  # do not leave the other threads waiting for this pass's collective
-                    ar_turn[0] = AR_ABORT
-                    ar_cv.notify_all()
-
-        th = [threading.Thread(target=worker, args=(j,)) for j in range(min(jobs, n_steps))]
-        for t_ in th:
-            t_.start()
-        for t_ in th:
-            t_.join()
-        if err:
-            raise err[0]
-        return res
-
-    run(max(args.warmup, jobs))  # every engine warmed (buffers sized, code loaded)
+    for sd in warm_seeds:
+        one_pass(engine, sd, id_base[sd], world > 1)
+    launches0 = engine.stats()["n_launches"]
     if dist is not None:
         dist.barrier()
+    res, pass_s = [], []
     t0 = time.time()
-    res = run(args.steps)
+    for sd in timed_seeds:
+        tp = time.time()
+        res.append(one_pass(engine, sd, id_base[sd], world > 1))
+        pass_s.append(time.time() - tp)
     if dist is not None:
         dist.barrier()
     elapsed = time.time() - t0
-    kern_ms = sum(r[0]["last_kernel_ms"] for r in res)
-    steps_tot = sum(r[0]["last_steps"] for r in res)
-    tracked = sum(r[0]["n_tracked"] for r in res)
-    children = sum(r[0]["n_children"] for r in res)
-    emit_ms = 0.0 if args.host_emit else sum(r[0]["last_emit_ms"] for r in res)
-    big_ms = sum(r[0]["max_launch_ms"] for r in res)
-    big_steps = sum(r[0]["max_launch_steps"] for r in res)
-    pass_s = sorted(r[3] for r in res)
-    longest_life = max(r[0]["max_photon_steps"] for r in res)
-    launches = sum(e_.stats()["n_launches"] for e_ in engines)
-    tmax, total = elapsed, n * args.steps
+    n_rank = sum(r[0] for r in res)
+    tmax, total = elapsed, n_rank
     if dist is not None:
         tm = torch.tensor([elapsed], dtype=torch.float64)
-        tt = torch.tensor([float(total)], dtype=torch.float64)
+        tt = torch.tensor([float(n_rank)], dtype=torch.float64)
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
         tmax, total = float(tm[0]), int(tt[0])
+
+    overlapped = None
+    if rank == 0 and overlap > 1:
+        overlapped = overlapped_throughput(model, overlap, z0, z1)
     if rank == 0:
-        k_ms = kern_ms / args.steps
-        # per launch, for the dominant track_kernel launch of each step (rocprof's longest dispatches)
-        achieved = big_steps * ALG_BYTES_PER_STEP / (big_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.pmc_summary, args.steps + max(args.warmup, jobs))
+        sts = [r[1] for r in res]
+        launches = res[-1][1]["n_launches"] - launches0
+        kern_ms = sum(s["last_kernel_ms"] for s in sts)
+        steps_tot = sum(s["last_steps"] for s in sts)
+        big_ms = sum(s["max_launch_ms"] for s in sts)
+        big_steps = sum(s["max_launch_steps"] for s in sts)
+        emit_ms = sum(s["last_emit_ms"] for s in sts)
+        cnt = fp64_count()
+        flops_step = cnt["flops_per_step"] if cnt else None
+        traffic = pmc_traffic(args.pmc_summary)
+        achieved_tf = big_steps * flops_step / (big_ms * 1e-3) / 1e12 if flops_step else None
+        alg_gbs = big_steps * ALG_BYTES_PER_STEP / (big_ms * 1e-3) / 1e9
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             try:
-                cpu = cpu_baseline(path, photon_n_job, photons, args.cpu_seconds)
+                ph = model.emit(seed=SEED0, z0=z0, z1=z1, threads=threads)
+                cpu = cpu_baseline(path, photon_n_job, ph, args.cpu_seconds)
             except Exception as ex:  # the baseline is reported beside the product, never part of it
                 cpu = {"value": None, "error": repr(ex)}
+        srt = sorted(pass_s)
         out = {
-            "metric": "superphotons/sec on dump019-class HARM dump (photon_n=1e6 per GPU)"
-                      + (" [transport only]" if args.host_emit else ""),
+            "metric": "superphotons/sec on dump019-class HARM dump (photon_n=1e6 per run_simulation)",
             "value": total / tmax,
             "unit": "superphotons/s",
             "n_gpus": world,
@@ -298,40 +269,90 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": tmax / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"synthetic dump019-class {args.grid}x{args.grid} MKS HARM dump, photon_n="
-                                   f"{int(args.photon_n):g} per GPU (one photon_n x {world} job zone-sharded), "
-                                   f"mass_unit=4e19, {n} emitted superphotons on rank 0",
-                       "photon_n_per_gpu": int(args.photon_n), "grid": f"{args.grid}x{args.grid}",
-                       "superphotons_rank0": n, "parallelism": f"zone shards x{world}, RCCL spectrum all-reduce"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "achieved_sustained": steps_tot * ALG_BYTES_PER_STEP / tmax / 1e9,
-                         "frac_sustained": steps_tot * ALG_BYTES_PER_STEP / tmax / 1e9 / HBM_PEAK_GBS,
+                                   f"{photon_n_job:g} run_simulation passes (seeds {SEED0}..{SEED0 + args.steps - 1}), "
+                                   f"mass_unit=4e19, zone-sharded over {world} GPU(s)",
+                       "photon_n_job": photon_n_job, "grid": f"{args.grid}x{args.grid}",
+                       "superphotons_per_pass_rank0": n_rank // max(1, args.steps),
+                       "parallelism": f"zone shards x{world}, RCCL spectrum all-reduce"},
+            "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": achieved_tf / FP64_PEAK_TFS if achieved_tf else None,
                          "traffic": traffic,
-                         "note": f"dominant track_kernel launch: {ALG_BYTES_PER_STEP} algorithmic B per transport step x "
-                                 f"{big_steps // args.steps} steps / {big_ms / args.steps:.1f} ms (HIP events on the "
-                                 f"engine stream, {jobs} passes in flight); all launches of a step: "
-                                 f"{steps_tot // args.steps} steps in {k_ms:.1f} ms; sustained over the timed window "
-                                 f"{steps_tot * ALG_BYTES_PER_STEP / tmax / 1e9:.0f} GB/s; the kernel is "
-                                 f"fp64-VALU/latency bound -- DESIGN.md"},
+                         "flops_per_step": flops_step,
+                         "transcendentals_per_step": cnt.get("transcendentals_per_step") if cnt else None,
+                         "hbm_algorithmic_gbs": alg_gbs, "hbm_frac": alg_gbs / HBM_PEAK_GBS,
+                         "note": f"dominant track_kernel launch per pass (alone on the GPU): "
+                                 f"{big_steps // args.steps} transport steps in {big_ms / args.steps:.1f} ms "
+                                 f"(HIP events on the engine stream) x {flops_step} counted FP64 flops/step "
+                                 f"({FP64_COUNT.replace(REPO + '/', '')}); HBM view: {ALG_BYTES_PER_STEP} algorithmic "
+                                 f"B/step -> {alg_gbs:.0f} GB/s; traffic = PMC FETCH(x2)+WRITE bytes per dominant "
+                                 f"launch (null unless --pmc-summary)"},
             "cpu_baseline": cpu,
-            "detail": {"transport_steps_per_s": steps_tot / (kern_ms * 1e-3), "kernel_ms_per_step": k_ms,
-                       "passes_in_flight": jobs,
-                       "pass_latency_s": {"min": pass_s[0], "median": pass_s[len(pass_s) // 2], "max": pass_s[-1]},
-                       "single_pass_rate": n / pass_s[len(pass_s) // 2],
-                       "longest_photon_life_steps": longest_life,
-                       "emit_ms_per_step": emit_ms / args.steps,
-                       "emission": "host (untimed)" if args.host_emit else "device (timed)",
-                       "tracked_per_step": tracked // args.steps, "children_per_step": children // args.steps,
-                       "launches_total": launches, "init_s": t_init, "emit_s": t_emit},
+            "detail": {"pass_s": {"min": srt[0], "median": srt[len(srt) // 2], "max": srt[-1],
+                                  "all": [round(v, 4) for v in pass_s]},
+                       "transport_steps_per_s": steps_tot / (kern_ms * 1e-3), "kernel_ms_per_pass": kern_ms / args.steps,
+                       "dominant_launch_ms_per_pass": big_ms / args.steps,
+                       "emit_ms_per_pass": emit_ms / args.steps,
+                       "longest_photon_life_steps": max(s["max_photon_steps"] for s in sts),
+                       "tracked_per_pass": sum(s["n_tracked"] for s in sts) // args.steps,
+                       "children_per_pass": sum(s["n_children"] for s in sts) // args.steps,
+                       "recorded_per_pass": sum(r[2] for r in res) // args.steps,
+                       "launches_per_pass": launches / args.steps,
+                       "overlapped": overlapped,
+                       "init_s": t_init, "count_s": t_count},
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def overlapped_throughput(model, jobs: int, z0: int, z1: int):
+    """detail only: `jobs` independent passes (distinct seeds) in flight at once, one engine + host
+    thread each, on this rank's zones -- what the device sustains when runs share it"""
+    import threading
+    engines = [G.Engine(model, device=int(os.environ.get("LOCAL_RANK", "0"))) for _ in range(jobs)]
+    for e in engines:
+        e.emit_setup(model)
+    err, counts = [], [0] * jobs
+
+    def run(j, seed):
+        try:
+            e = engines[j]
+            e.reset()
+            e.set_option(G.OPT_SEED, seed)
+            e.set_option(G.OPT_ID_BASE, 0)
+            ptr, n = e.emit(seed=seed, z0=z0, z1=z1)
+            e.track_device(ptr, n)
+            st = e.stats()
+            if st["n_dropped"] or st["n_abandoned"]:
+                raise RuntimeError("overlapped pass lost photons")
+            e.finish()
+            counts[j] += n
+        except Exception as ex:
+            err.append(ex)
+
+    def phase(seed0):
+        th = [threading.Thread(target=run, args=(j, seed0 + j)) for j in range(jobs)]
+        for t_ in th:
+            t_.start()
+        for t_ in th:
+            t_.join()
+
+    phase(OVERLAP_SEED0)  # warm every engine
+    counts[:] = [0] * jobs
+    t = time.time()
+    phase(OVERLAP_SEED0 + jobs)
+    el = time.time() - t
+    for e in engines:
+        e.close()
+    if err:
+        return {"error": repr(err[0])}
+    return {"passes_in_flight": jobs, "passes": jobs, "superphotons_per_s": sum(counts) / el, "wall_s": el,
+            "note": "independent passes (distinct seeds) sharing the GPU; not the reference's per-run rate"}
 
 
 if __name__ == "__main__":

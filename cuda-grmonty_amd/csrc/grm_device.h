@@ -42,8 +42,7 @@ constexpr int N_TH_BINS = GRM_N_TH_BINS, N_E_BINS = GRM_N_E_BINS;
  * The transport step's divisors are finite, normal, non-zero physical quantities, so the hot path
  * divides with v_rcp_f64 + two Newton steps + one residual correction (7 ops, <= 1 ulp from the
  * correctly rounded quotient -- below the fp-contraction differences the CPU reference already has
- * from one compiler to another).  -DGRM_EXACT_DIV restores plain '/' (A/B builds). */
-#ifndef GRM_EXACT_DIV
+ * from one compiler to another). */
 __device__ __forceinline__ double frcp(double b) {
     double r = __builtin_amdgcn_rcp(b);
     double e = fma(-b, r, 1.0);
@@ -62,19 +61,9 @@ __device__ __forceinline__ double fratio_tol(double a, double b) {
     r = fma(r, fma(-b, r, 1.0), r);
     return fabs(a * r);
 }
-#else
-__device__ __forceinline__ double frcp(double b) { return 1.0 / b; }
-__device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
-__device__ __forceinline__ double fratio_tol(double a, double b) { return fabs(a / b); }
-#endif
 /* a / b for a kernel-argument divisor b with host reciprocal ib: one multiply (<= 1 ulp from a / b;
- * only grid / table coordinates go through it, whose interpolants are continuous across cells).
- * -DGRM_DIV_PARAMS restores the division (A/B builds). */
-#ifndef GRM_DIV_PARAMS
+ * only grid / table coordinates go through it, whose interpolants are continuous across cells). */
 __device__ __forceinline__ double udiv(double a, double, double ib) { return a * ib; }
-#else
-__device__ __forceinline__ double udiv(double a, double b, double) { return fdiv(a, b); }
-#endif
 
 /* Kernel-argument block: everything uniform across lanes (lands in SGPRs). */
 struct Params {
@@ -173,14 +162,8 @@ struct Trig {
  * one (agreement with sin/cos of the pi-multiplied argument to a few ulp) */
 __device__ __forceinline__ void trig_at(const Params &P, const double x[4], Trig &T) {
     T.r1 = exp(x[1]);
-#ifndef GRM_TRIG_GENERAL
     sincospi(2.0 * x[2], &T.s2x, &T.c2x);
     sincospi(x[2] + ((1.0 - P.h_slope) / (2.0 * kPi)) * T.s2x, &T.sth, &T.cth);
-#else
-    sincos(2.0 * kPi * x[2], &T.s2x, &T.c2x);
-    const double th = kPi * x[2] + ((1.0 - P.h_slope) / 2.0) * T.s2x;
-    sincos(th, &T.sth, &T.cth);
-#endif
 }
 
 /* non-zero g_mu,nu of MKS Kerr + g^{00}, g^{01} (g^{02} = g^{03} = 0) */
@@ -252,12 +235,8 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
     const double fac2 = a2 + 2.0 * r2 + a2 * c2th;
     const double fac3 = a2 + r1 * (-2.0 + r1);
     const double i_r1rho23 = frcp(r1) * irho23;
-#ifdef GRM_FAC2_RCP
-    const double i_sth = frcp(sth), ifac2 = frcp(fac2);
-#else
     /* fac2 = a^2 + 2 r^2 + a^2 cos(2 theta) = 2 rho^2: one reciprocal fewer (agreement to an ulp) */
     const double i_sth = frcp(sth), ifac2 = 0.5 * irho2;
-#endif
 
     C.c[0][0] = 2.0 * r1 * fac1_rho23;
     C.c[0][1] = r1 * (2.0 * r1 + rho2) * fac1_rho23;
@@ -330,15 +309,6 @@ __device__ __forceinline__ void init_dkdlam(const Params &P, const double x[4], 
 
 /* harm_model.cpp:1620-1630 */
 __device__ __forceinline__ double step_size(const Params &P, const double x[4], const double k[4]) {
-#ifdef GRM_STEP_SEVEN_DIV
-    const double dl_x_1 = fdiv(STEP_EPS * x[1], fabs(k[1]) + EPS);
-    const double dl_x_2 = fdiv(STEP_EPS * fmin(x[2], P.xe2 - x[2]), fabs(k[2]) + EPS);
-    const double dl_x_3 = fdiv(STEP_EPS, fabs(k[3]) + EPS);
-    const double i1 = frcp(fabs(dl_x_1) + EPS);
-    const double i2 = frcp(fabs(dl_x_2) + EPS);
-    const double i3 = frcp(fabs(dl_x_3) + EPS);
-    return frcp(i1 + i2 + i3);
-#else
     /* 1 / (|a / b| + EPS) = b / (|a| + EPS b) with b = |k| + EPS > 0: four divisions instead of
      * seven (same value to rounding; a = 0 still gives 1 / EPS) */
     const double b1 = fabs(k[1]) + EPS, b2 = fabs(k[2]) + EPS, b3 = fabs(k[3]) + EPS;
@@ -346,20 +316,12 @@ __device__ __forceinline__ double step_size(const Params &P, const double x[4], 
     const double i2 = fdiv(b2, fabs(STEP_EPS * fmin(x[2], P.xe2 - x[2])) + EPS * b2);
     const double i3 = fdiv(b3, STEP_EPS + EPS * b3);
     return frcp(i1 + i2 + i3);
-#endif
 }
 
 /* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
- * predicate of :1279 and the new energy e_1; leaves Gcov at the new x in G. */
-struct NoPrefetch {
-    __device__ __forceinline__ void operator()(const double *) const {}
-};
-
-/* `pre(x)` runs as soon as the new position is known (before the connection and the corrector),
- * so the caller can issue the fluid gather at x early and let this attempt's VALU work hide it. */
-template <class Pre = NoPrefetch>
+ * predicate of :1279 and the new energy e_1; leaves Trig and Gcov at the new x in T, G. */
 __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
-                                             double dl, double &e_1, Trig &T, Gcov &G, Pre &&pre = Pre()) {
+                                             double dl, double &e_1, Trig &T, Gcov &G) {
     const double dl_2 = 0.5 * dl;
     double kp[4];
 #pragma unroll
@@ -369,7 +331,6 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
         kp[i] = k[i] + d;
         x[i] += k[i] * dl;
     }
-    pre(x);
     trig_at(P, x, T);
     Conn C;
     connection(P, T, C);

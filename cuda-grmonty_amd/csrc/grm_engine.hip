@@ -38,25 +38,13 @@ using namespace grm;
 
 namespace {
 
-/* One workgroup per CU, BLOCK / 256 waves per SIMD.  512 lanes (two waves per SIMD, 256 VGPRs each)
- * is the default: the second wave issues while the first waits on a gather or a scalar/branch slot,
- * +20% over 256 lanes (one wave per SIMD, 256 VGPRs + AGPRs) measured on MI355X. */
-#ifndef GRM_BLOCK
+/* One workgroup per CU of 512 lanes: two waves per SIMD at 256 VGPRs each -- the second wave issues
+ * while the first waits on a gather or a scalar/branch slot (+20% over one wave per SIMD, measured
+ * on MI355X).  The per-lane state copies and per-step lane fields take the LDS, so the
+ * spectrum goes to a per-workgroup slice in HBM (L2 atomics). */
 #define GRM_BLOCK 512
-#endif
-#ifndef GRM_WAVES_PER_SIMD
-#define GRM_WAVES_PER_SIMD (GRM_BLOCK / 256)
-#endif
-/* 256 lanes per CU: spectrum in LDS.  512 lanes (two waves per SIMD): the LDS state copies take
- * 90 KB, so the spectrum goes to a per-workgroup slice in HBM (L2 atomics).
- * GRM_PREFETCH=1 issues the fluid gather during the push (its 64 VGPRs held across the connection
- * and corrector); measured 2.5% slower than gathering at the use at one wave per SIMD. */
-#define GRM_SPEC_LDS (GRM_BLOCK <= 256)
-#ifndef GRM_PREFETCH
-#define GRM_PREFETCH 0
-#endif
 constexpr int BLOCK = GRM_BLOCK;
-constexpr int MIN_WAVES_PER_SIMD = GRM_WAVES_PER_SIMD;
+constexpr int MIN_WAVES_PER_SIMD = BLOCK / 256;
 constexpr int STACK_DEPTH = 16;                 /* scatter-request slots per lane ... */
 constexpr int WSTACK_CAP = 64 * STACK_DEPTH;    /* ... pooled into one stack per wave (208 KB of HBM) */
 
@@ -129,17 +117,11 @@ struct Ctl {
     unsigned long long stuck_cap, *stuck_count;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
-#ifndef GRM_REFRESH_TRIPS
-#define GRM_REFRESH_TRIPS 64
-#endif
-constexpr unsigned REFRESH_TRIPS = GRM_REFRESH_TRIPS; /* counter flush + bias refresh + watchdog period (power of 2) */
+constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
 
-/* Per-step (or rarer) lane fields: registers in the one-wave build; in the two-wave build
- * (GRM_LANE_LDS) an LDS column per lane ([field][lane], conflict-free), read and written where used
- * -- what brings the kernel's register demand under the 256 VGPRs two waves per SIMD allow. */
-#ifndef GRM_LANE_LDS
-#define GRM_LANE_LDS (GRM_BLOCK > 256)
-#endif
+/* Per-step (or rarer) lane fields: an LDS column per lane ([field][lane], conflict-free), read and
+ * written where used -- what brings the kernel's register demand under the 256 VGPRs two waves per
+ * SIMD allow. */
 #define GRM_LANE_XFIELDS(X)                                                                          \
     X(tau_abs, 0) X(tau_scatt, 1) X(alpha_scatti, 2) X(alpha_absi, 3) X(bi, 4) X(fl_ne, 5)          \
     X(ph2_e0s, 6)     /* photon_2's e_0_s (its x^1..3, k, dk are in the ph2 LDS slot) */              \
@@ -151,7 +133,6 @@ constexpr int LANE_XFIELDS = 10;
     /* the lane's launch counters (widened and wave-reduced at exit) */                              \
     X(c_steps, 2) X(c_tracked, 3) X(c_primaries, 4) X(c_children, 5) X(c_nstep_max, 6) X(c_long, 7)
 constexpr int LANE_IFIELDS = 8;
-#if GRM_LANE_LDS
 /* [field][lane], indexed with threadIdx.x so that every access is one ds_read/ds_write_b64 with an
  * immediate offset (a generic pointer here would turn them into FLAT accesses, which also count in
  * vmcnt and cost a 64-bit address register each) */
@@ -161,7 +142,6 @@ __shared__ double s_lanex[LANE_XFIELDS * GRM_BLOCK];
 typedef __attribute__((address_space(3))) volatile double LdsDouble;
 __shared__ int s_lanei[LANE_IFIELDS * GRM_BLOCK];
 typedef __attribute__((address_space(3))) volatile int LdsInt;
-#endif
 
 /* hot photon state: lives in VGPRs (and, see above, LDS) for the photon's whole life */
 struct Lane {
@@ -174,21 +154,10 @@ struct Lane {
     int phase, depth;
     uint32_t pend;
     double dl, hlen;                      /* step size of this iteration; length being pushed */
-#if GRM_LANE_LDS
 #define X(name, i) \
     __device__ __forceinline__ LdsDouble &name() const { return ((LdsDouble *)s_lanex)[(i) * GRM_BLOCK + threadIdx.x]; }
 #define XI(name, i) \
     __device__ __forceinline__ LdsInt &name() const { return ((LdsInt *)s_lanei)[(i) * GRM_BLOCK + threadIdx.x]; }
-#else
-    double xf[LANE_XFIELDS];
-    int xif[LANE_IFIELDS];
-#define X(name, i)                                                           \
-    __device__ __forceinline__ double &name() { return xf[i]; }              \
-    __device__ __forceinline__ double name() const { return xf[i]; }
-#define XI(name, i)                                                          \
-    __device__ __forceinline__ int &name() { return xif[i]; }                \
-    __device__ __forceinline__ int name() const { return xif[i]; }
-#endif
     GRM_LANE_XFIELDS(X)
     GRM_LANE_IFIELDS(XI)
 #undef X
@@ -303,20 +272,14 @@ __device__ __forceinline__ void trace_end(const Ctl &C, const Cold *cold, const 
                     reason, -1, -1);
 }
 
-/* Workgroup-private spectrum and per-wave counter deltas in LDS.  record_super_photon's twelve
- * fp64 adds go to LDS (ds_add_f64) instead of global atomics: global float atomics execute at the
- * memory side and stay counted in the wave's in-order vmcnt for ~1-3k cycles, so every later load
- * of the wave (the next fluid gather) would wait for them.  The block adds its spectrum to the
- * global one once, at exit; counter deltas are flushed by each wave at its bias-refresh points.
- * Field f of a cell = field f of grm_spectrum_cell (e_0, never accumulated, is left out). */
+/* Workgroup-private spectrum slice (HBM, L2-resident: the twelve fp64 adds of record_super_photon
+ * are L2 atomics of this workgroup's CU only, never a cross-die line) and per-wave counter deltas in
+ * LDS.  The block adds its slice to the global spectrum once, at exit; counter deltas are flushed by
+ * each wave at its bias-refresh points.  Field f of a cell = field f of grm_spectrum_cell (e_0,
+ * never accumulated, is left out). */
 constexpr int SPEC_FIELDS = 12;
 constexpr int SPEC_LDS = N_TH_BINS * N_E_BINS * SPEC_FIELDS;
-#if GRM_SPEC_LDS
-__shared__ double s_spec[SPEC_LDS];
-__device__ __forceinline__ double *spec_slice(const Ctl &) { return s_spec; }
-#else
 __device__ __forceinline__ double *spec_slice(const Ctl &C) { return C.spec_blocks + (size_t)blockIdx.x * SPEC_LDS; }
-#endif
 __shared__ unsigned long long s_cnt[BLOCK / 64][4]; /* n_recorded, n_scatt, max tau bits, max flushed */
 
 __device__ __forceinline__ void flush_counters(const Ctl &C) {
@@ -540,11 +503,11 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const 
 }
 
 /* Two per-lane state copies live in LDS ([slot][lane], conflict-free 8-B words), 11 slots each:
- * x^1..x^3, k, dk/dlambda; their x^0 (and photon_2's e_0_s) stay in registers.
+ * x^1..x^3, k, dk/dlambda; photon_2's e_0_s is a lane field.
  *   ph2: photon_2 (harm_model.cpp:920-925), also the depth-0 backup of push_photon;
  *   bk:  the backup of push_photon at depth > 0 (x_cpy/k_cpy/dk_cpy, :1222-1228).
- * 2 x 11 x 8 B x 256 lanes + the 115 KB spectrum = 160 KB, one CU's LDS: no global memory
- * traffic on the halving path (a lane deep in halving runs alone at the end of a launch). */
+ * 2 x 11 x 8 B x 512 lanes = 88 KB (+ 40 KB of lane fields, 16 KB of lane ints): no global memory
+ * traffic on the halving path. */
 constexpr int LDS_DOUBLES_PER_LANE = 11;
 constexpr int WARM_GRID = 64; /* workgroups of the warm-up launch (batches of <= lanes/2 photons) */
 
@@ -637,12 +600,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             save_xkdk(bk, L);
         }
         double e_1;
-        const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -L.depth), e_1, T, G,
-#if GRM_PREFETCH
-                                       [&](const double *xn) { zone_fetch(P, xn, Z); });
-#else
-                                       NoPrefetch());
-#endif
+        const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -L.depth), e_1, T, G);
         TSTAMP(9);
         if (setup) {
             /* restore x, k exactly (a non-finite dk must not leak into them through 0 * dk) */
@@ -695,13 +653,8 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         if (!have_tg) {
             trig_at(P, L.x, T);
             gcov_from_trig(P, T, G);
-#if GRM_PREFETCH
-            zone_fetch(P, L.x, Z);
-#endif
         }
-#if !GRM_PREFETCH
         zone_fetch(P, L.x, Z);
-#endif
         Fluid F;
         fluid_from(P, L.x, G, Z, F);
         L.fl_ne() = F.n_e;
@@ -843,9 +796,6 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     __shared__ int s_wtop[BLOCK / 64];
     int *wtop = s_wtop + wave;
     if (lane_id == 0) *wtop = 0;
-#if GRM_SPEC_LDS
-    for (int i = threadIdx.x; i < SPEC_LDS; i += BLOCK) s_spec[i] = 0.0;
-#endif
     if (lane_id < 4) s_cnt[wave][lane_id] = 0;
     __syncthreads();
     Cold *cold = C.cold + gtid;
@@ -1056,13 +1006,9 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     __syncthreads();
     double *slice = spec_slice(C);
     for (int i = threadIdx.x; i < SPEC_LDS; i += BLOCK) {
-#if GRM_SPEC_LDS
-        const double v = slice[i];
-#else
         /* the slice was accumulated by L2 atomics; read it there and leave it zero for the next launch */
         const double v = __hip_atomic_load(slice + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v != 0.0) slice[i] = 0.0;
-#endif
         if (v != 0.0) unsafeAtomicAdd(reinterpret_cast<double *>(C.spec + i / SPEC_FIELDS) + i % SPEC_FIELDS, v);
     }
     /* wave-reduce the lane counters, one atomic per wave */
@@ -1137,7 +1083,7 @@ struct grm_engine {
     unsigned long long *d_waves = nullptr; /* [lanes / 64][4] per-wave record of the last launch */
     int64_t watchdog_ms = 60000;           /* per-launch watchdog (GRM_OPT_WATCHDOG_MS; 0 = off) */
     double *d_stuck = nullptr;             /* [STUCK_CAP][STUCK_WORDS] abandoned-photon records */
-    double *d_spec_blocks = nullptr;       /* per-workgroup spectrum slices (GRM_SPEC_LDS == 0) */
+    double *d_spec_blocks = nullptr;       /* per-workgroup spectrum slices */
     /* pinned host staging for the per-pass small transfers: resets are H2D copies from pin->zero and
      * readbacks land in pin->ctr / pin->word, all on the engine stream -- DMA engine transfers, where
      * pageable copies and hipMemset would each need a blit/fill kernel, i.e. a free CU, which with
@@ -1207,12 +1153,10 @@ int alloc_lanes(grm_engine *e) {
         if (e->d_waves) (void)hipFree(e->d_waves);
         e->d_waves = nullptr;
         HIPCHK(e, hipMalloc(&e->d_waves, lanes / 64 * 4 * sizeof(unsigned long long)));
-#if !GRM_SPEC_LDS
         if (e->d_spec_blocks) (void)hipFree(e->d_spec_blocks);
         e->d_spec_blocks = nullptr;
         HIPCHK(e, hipMalloc(&e->d_spec_blocks, (size_t)grid * SPEC_LDS * sizeof(double)));
         HIPCHK(e, hipMemset(e->d_spec_blocks, 0, (size_t)grid * SPEC_LDS * sizeof(double)));
-#endif
         e->lanes = lanes;
     }
     e->grid = grid;
@@ -1349,6 +1293,13 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     }
     DevCounters h;
     if (read_counters(e, h)) return -1;
+    if (h.n_dropped) {
+        /* a scattered child that fit neither the wave stack nor the overflow pool is lost: the
+         * spectrum of this call would be incomplete, so the call fails */
+        e->err = std::to_string(h.n_dropped) + " scattered children dropped (overflow pool of " +
+                 std::to_string(e->ovf_cap) + " full); results of this call are incomplete";
+        return -1;
+    }
     e->stats.kernel_ms += ms_total;
     e->stats.last_kernel_ms += ms_total;
     e->stats.last_steps += h.n_steps - steps_before;

@@ -358,7 +358,7 @@ class Engine:
         out = np.zeros((256, 16), dtype=np.float64)
         n = self.L.grm_engine_debug_stuck(self.h, _ptr(out), 256)
         if n < 0:
-            raise RuntimeError(self.error())
+            raise RuntimeError(self.L.grm_engine_last_error(self.h).decode())
         return out[:n]
 
     def allreduce(self):

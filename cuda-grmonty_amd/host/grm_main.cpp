@@ -163,7 +163,10 @@ int main(int argc, char **argv) {
     std::vector<grm_spectrum_cell> spec(GRM_N_TH_BINS * GRM_N_E_BINS);
     uint64_t n_rec = 0, n_scatt = 0;
     double max_tau = 0.0;
-    grm_engine_finish(e, spec.data(), &n_rec, &n_scatt, &max_tau);
+    if (grm_engine_finish(e, spec.data(), &n_rec, &n_scatt, &max_tau)) {
+        std::fprintf(stderr, "[error] spectrum readback: %s\n", grm_engine_last_error(e));
+        return 1;
+    }
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     info("Final rate %.2f ph/s", created / el);
     info("Super photons:");
@@ -171,7 +174,10 @@ int main(int argc, char **argv) {
     info("\tscattered: %llu", (unsigned long long)n_scatt);
     info("\trecorded: %llu", (unsigned long long)n_rec);
     grm_stats st;
-    grm_engine_stats(e, &st);
+    if (grm_engine_stats(e, &st)) {
+        std::fprintf(stderr, "[error] engine stats: %s\n", grm_engine_last_error(e));
+        return 1;
+    }
     info("\ttransport steps: %llu (%.3g steps/s in kernel)", (unsigned long long)st.n_steps,
          st.n_steps / (st.kernel_ms * 1e-3 + 1e-30));
     if (!spec_path.empty()) {

@@ -40,12 +40,12 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
     e.reset()
     if os.environ.get("IDB"):
         e.set_option(G.OPT_ID_BASE, int(os.environ["IDB"].split(",")[rep]))
-    if os.environ.get("SEED"):
-        e.set_option(G.OPT_SEED, int(os.environ["SEED"]) + rep)
+    seed = int(os.environ.get("SEED", "123")) + rep  # distinct Monte Carlo pass per rep
+    e.set_option(G.OPT_SEED, seed)
     t = time.time()
     try:
         if dev_emit:
-            p, n_dev = e.emit(seed=123)
+            p, n_dev = e.emit(seed=seed)
             e.track_device(p, n_dev)
         else:
             e.track(ph)
@@ -58,10 +58,11 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
     wall = time.time() - t
     spec, nr, ns, mt = e.finish()
     st = e.stats()
-    print(f"rep {rep}: wall {wall:.3f}s kernel {st['last_kernel_ms']:.1f}ms steps {st['last_steps']} "
+    n_em = n_dev if dev_emit else len(ph)
+    print(f"rep {rep} seed {seed}: wall {wall:.3f}s kernel {st['last_kernel_ms']:.1f}ms steps {st['last_steps']} "
           f"({st['last_steps'] / st['last_kernel_ms'] / 1e3:.3g} Msteps/s) tracked {st['n_tracked']} "
           f"children {st['n_children']} overflow {st['n_overflow']} launches {st['n_launches']} "
-          f"rate {len(ph) / (st['last_kernel_ms'] * 1e-3):.4g} ph/s rec {nr} scatt {ns} | longest launch "
+          f"rate {n_em / wall:.4g} ph/s rec {nr} scatt {ns} | longest launch "
           f"{st['max_launch_ms']:.1f}ms ({st['max_launch_steps']} steps) longest life {st['max_photon_steps']} steps, "
           f"{st['n_long_photons']} lives > 1e5 steps, {st['n_nan_photons']} NaN-ended", flush=True)
     wv = e.debug_waves().astype(np.float64)
