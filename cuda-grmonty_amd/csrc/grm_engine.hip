@@ -564,27 +564,98 @@ __device__ bool init_photon(const Ctl &C, const Cold *cold, Lane &L, const Slot 
     return true;
 }
 
+/* Head of a geodesic step (phase 0): stop test, photon_2, step size (harm_model.cpp:919-927).
+ * false = the photon's life ended. */
+__device__ __forceinline__ bool trip_begin(const Params &P, const Ctl &C, Lane &L, Cold *cold, const Slot &ph2) {
+    if (stop_criterion(P, L)) {
+        end_of_life(P, C, cold, L);
+        return false;
+    }
+    /* photon_2 (:920-925) -- also the depth-0 backup of the push */
+    store_ph2(ph2, L);
+    L.dl = step_size(P, L.x, L.k);
+    L.hlen = L.dl;
+    L.depth = 0;
+    L.pend = 0;
+    L.phase = 1;
+    return true;
+}
+
+/* lane `src`'s value of v (src wave-uniform) */
+__device__ __forceinline__ double bcast(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, src), hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+/* Tail speculation.  A wave whose only work left is ONE photon (the pool is drained and its stack
+ * empty) completes that photon's current push -- push_photon's halving recursion,
+ * harm_model.cpp:1217-1289 -- with all its lanes: from the start state of every sub-step the owner
+ * attempts depth d and idle lane r attempts depth d + r, at once.  The serial walk would attempt d,
+ * then (restored to the same start state) d + 1, ... until one passes or depth MAX_SUBDIV accepts
+ * whatever it gets; each of these attempts is made here from bit-identical inputs, so the shallowest
+ * accepted one IS the serial walk's sub-step, its failed shallower attempts become the pending
+ * second halves they would have left, and the walk goes on from the accepted state.  One round per
+ * accepted sub-step instead of one trip per attempt: the photons that halve to depth 7 on every
+ * step (255 attempts for 128 sub-steps) -- the last photons of a pass -- run ~2x faster.
+ * Called by the whole wave (converged); `owner` is wave-uniform.  Every lane's copy of the push
+ * state (x, k, dk/dlambda, e_0_s, hlen, depth, pend) follows the owner's; only the owner's is used. */
+__device__ __forceinline__ void halving_walk(const Params &P, Lane &L, int owner) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int rank = lane == owner ? 0 : (lane < owner ? lane + 1 : lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        L.x[i] = bcast(L.x[i], owner);
+        L.k[i] = bcast(L.k[i], owner);
+        L.dk[i] = bcast(L.dk[i], owner);
+    }
+    L.e_0_s = bcast(L.e_0_s, owner);
+    L.hlen = bcast(L.hlen, owner);
+    L.depth = __builtin_amdgcn_readlane(L.depth, owner);
+    L.pend = (uint32_t)__builtin_amdgcn_readlane((int)L.pend, owner);
+    while (true) {
+        if (!(L.x[1] < P.xs1)) {
+            /* every lane attempts in place from the same start state; the winner's result is then
+             * broadcast over all of them */
+            const int d = L.depth + rank;
+            double e_1 = 0.0;
+            bool ok = false;
+            if (d <= MAX_SUBDIV) {
+                Trig T;
+                Gcov G;
+                const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -d), e_1, T, G);
+                ok = !fail || d == MAX_SUBDIV;
+            }
+            /* the owner's attempt if it passed, else the shallowest passing helper (helper depth grows
+             * with lane index); some lane passes, since 63 helpers cover every depth to MAX_SUBDIV */
+            const unsigned long long acc = __ballot(ok);
+            const int w = ((acc >> owner) & 1ull) ? owner : __ffsll((long long)acc) - 1;
+            const int dw = __builtin_amdgcn_readlane(d, w);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                L.x[i] = bcast(L.x[i], w);
+                L.k[i] = bcast(L.k[i], w);
+                L.dk[i] = bcast(L.dk[i], w);
+            }
+            L.e_0_s = bcast(e_1, w);
+            L.pend |= ((2u << dw) - 1u) & ~((2u << L.depth) - 1u); /* second halves at depths depth+1..dw */
+            L.depth = dw;
+        }
+        if (L.pend == 0) break;
+        L.depth = 31 - __builtin_clz(L.pend);
+        L.pend &= ~(1u << L.depth);
+    }
+}
+
 /* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
  * completed a step, the rest of the while-loop body of track_super_photon
  * (harm_model.cpp:919-1063).  A lane that has to halve its step (push_photon's recursion,
  * :1279-1285) spends extra trips while the other lanes of the wave keep stepping, instead of the
- * whole wave waiting for the deepest halving tree.  Returns false when the photon's life ended. */
+ * whole wave waiting for the deepest halving tree.  `walked`: halving_walk has just completed this
+ * lane's push (its phase-0 block ran before it).  Returns false when the photon's life ended. */
 __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *wstack, int *wtop,
-                               const Slot &ph2,
-                               const Slot &bk, double bias_d) {
-    if (L.phase == 0) {
-        if (stop_criterion(P, L)) {
-            end_of_life(P, C, cold, L);
-            return false;
-        }
-        /* photon_2 (:920-925) -- also the depth-0 backup of the push */
-        store_ph2(ph2, L);
-        L.dl = step_size(P, L.x, L.k);
-        L.hlen = L.dl;
-        L.depth = 0;
-        L.pend = 0;
-        L.phase = 1;
-    }
+                               const Slot &ph2, const Slot &bk, double bias_d, bool walked) {
+    if (L.phase == 0 && !trip_begin(P, C, L, cold, ph2)) return false;
     TSTAMP(8);
     /* one attempt of push_photon at the current node of the halving tree (:1217-1289).  A lane in
      * set-up (phase 3) makes a zero-length attempt instead: x and k stay, the corrector's first pass
@@ -595,7 +666,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     Gcov G;
     ZoneFetch Z;
     bool have_tg = false;
-    if (setup || !(L.x[1] < P.xs1)) {
+    if (!walked && (setup || !(L.x[1] < P.xs1))) {
         if (L.depth > 0) {
             save_xkdk(bk, L);
         }
@@ -978,8 +1049,27 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             continue;
         }
         wait_trips = 0;
+        /* tail speculation (halving_walk): this wave's only work left is one photon in a push */
+        bool walked = false, ended = false;
+        if (pool_done && !warm) {
+            const unsigned long long act = __ballot(active);
+            if (__popcll(act) == 1 && *wtop == 0) {
+                const int owner = __ffsll((long long)act) - 1;
+                int walk = 0;
+                if (active) {
+                    if (L.phase == 0 && !trip_begin(P, C, L, cold, ph2))
+                        ended = true;
+                    else
+                        walk = (L.phase == 1 || L.phase == 2) ? 1 : 0;
+                }
+                if (__builtin_amdgcn_readlane(walk, owner)) {
+                    halving_walk(P, L, owner);
+                    walked = true;
+                }
+            }
+        }
         if (active) {
-            active = transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d);
+            active = !ended && transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked);
             if (!active) {
                 L.c_nstep_max() = max((int)L.c_nstep_max(), L.n_step);
                 L.c_long() += L.n_step > 100000 ? 1 : 0;
@@ -1031,11 +1121,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         atomicAdd(&C.ctr->n_children, w_children);
         if (w_long) atomicAdd(&C.ctr->n_long, w_long);
         atomicMax(&C.ctr->max_nstep, w_nstep_max);
-        unsigned long long *wr = C.waves + (gtid >> 6) * 4;
-        wr[0] = rt_start;
-        wr[1] = __builtin_amdgcn_s_memrealtime();
-        wr[2] = wave_trips;
-        wr[3] = w_tracked;
+        if (C.waves) {
+            unsigned long long *wr = C.waves + (gtid >> 6) * 4;
+            wr[0] = rt_start;
+            wr[1] = __builtin_amdgcn_s_memrealtime();
+            wr[2] = wave_trips;
+            wr[3] = w_tracked;
+        }
     }
 }
 
@@ -1196,7 +1288,6 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     C.trace_cap = e->trace_cap;
     C.trace_count = e->d_small + 3;
     C.timing = e->d_timing;
-    C.waves = e->d_waves;
     C.refill_min = e->refill_min;
     C.child_min = e->child_min;
     C.lanes = (int)e->lanes;
@@ -1250,6 +1341,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
         }
         C.ovf = e->d_ovf[dst];
         C.ovf_count = e->d_small + 1 + dst;
+        /* the per-wave record is kept of the first launch on the full grid (the bulk of a call) */
+        C.waves = (pass == 0 && grid == e->grid) ? e->d_waves : nullptr;
         if (pass > 0) {
             C.pool = e->d_ovf[src];
             C.pool_kind = 1;

@@ -14,7 +14,8 @@ git -C "$R" show "$rev:include/grmonty_amd.h" > "$D/include/grmonty_amd.h"
 sed -i 's|"../../include/grmonty_amd.h"|"../include/grmonty_amd.h"|' "$D/csrc/"*.h "$D/csrc/"*.hip
 make -s -C "$R/cuda-grmonty_amd" build/grm_host.o
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -mllvm -disable-machine-licm"
-for f in grm_engine grm_probe grm_emit; do
+/opt/rocm/bin/hipcc $FL -mllvm -amdgpu-sched-strategy=iterative-ilp $VFLAGS -c "$D/csrc/grm_engine.hip" -o "$D/grm_engine.o" &
+for f in grm_probe grm_emit; do
   /opt/rocm/bin/hipcc $FL -c "$D/csrc/$f.hip" -o "$D/$f.o" &
 done
 wait
