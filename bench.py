@@ -131,6 +131,19 @@ def cpu_baseline(path: str, photon_n: int, photons: np.ndarray, seconds: float):
                       f"host core; the reference's own CPU build is not buildable here (DESIGN.md §3)"}
 
 
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def committed_traffic():
+    """HBM bytes per dominant track_kernel launch measured by rocprofv3 PMC passes over this same
+    bench command (tools/traffic_summary.py -> profiles/pmc_traffic.json), or None"""
+    try:
+        with open(PMC_TRAFFIC) as fh:
+            return json.load(fh)["bytes_per_dominant_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def pmc_traffic(path: str):
     """HBM bytes per dominant track_kernel dispatch from rocprofv3 --pmc counter CSVs (FETCH_SIZE and
     WRITE_SIZE in KB, from separate passes; gfx950 FETCH_SIZE reports half of wide streaming reads ->
@@ -249,7 +262,7 @@ def main():
         emit_ms = sum(s["last_emit_ms"] for s in sts)
         cnt = fp64_count()
         flops_step = cnt["flops_per_step"] if cnt else None
-        traffic = pmc_traffic(args.pmc_summary)
+        traffic = pmc_traffic(args.pmc_summary) if args.pmc_summary else committed_traffic()
         achieved_tf = big_steps * flops_step / (big_ms * 1e-3) / 1e12 if flops_step else None
         alg_gbs = big_steps * ALG_BYTES_PER_STEP / (big_ms * 1e-3) / 1e9
         cpu = None
@@ -290,7 +303,8 @@ def main():
                                  f"(HIP events on the engine stream) x {flops_step} counted FP64 flops/step "
                                  f"({FP64_COUNT.replace(REPO + '/', '')}); HBM view: {ALG_BYTES_PER_STEP} algorithmic "
                                  f"B/step -> {alg_gbs:.0f} GB/s; traffic = PMC FETCH(x2)+WRITE bytes per dominant "
-                                 f"launch (null unless --pmc-summary)"},
+                                 f"launch (--pmc-summary CSVs of this run, else profiles/pmc_traffic.json: the PMC passes of this bench "
+                                 f"command, tools/traffic_summary.py)"},
             "cpu_baseline": cpu,
             "detail": {"pass_s": {"min": srt[0], "median": srt[len(srt) // 2], "max": srt[-1],
                                   "all": [round(v, 4) for v in pass_s]},

@@ -104,6 +104,7 @@ SIGNATURES = {
     "grm_model_emit": (C.c_int64, [VP, C.c_uint64, C.c_int64, C.c_int64, VP, C.c_size_t, C.c_int]),
     "grm_model_zone_weights": (C.c_int, [VP, DP]),
     "grm_write_spectrum": (C.c_int, [VP, VP, C.c_char_p, DP]),
+    "grm_write_spectrum_stats": (C.c_int, [VP, VP, C.c_char_p]),
     "grm_model_zone_table": (C.c_int, [VP, C.c_int64, C.c_int64, VP, C.c_int]),
     "grm_engine_emit_setup": (C.c_int, [VP, VP, C.c_int64, DP, DP]),
     "grm_engine_emit_setup_from_model": (C.c_int, [VP, VP]),
@@ -243,6 +244,11 @@ class Model:
         if self.L.grm_write_spectrum(self.h, _ptr(s), path.encode() if path else None, o.ctypes.data_as(DP)) != 0:
             raise IOError(self.L.grm_model_last_error().decode())
         return dict(luminosity=o[0], max_tau_scatt=o[1])
+
+    def write_spectrum_stats(self, spectrum: np.ndarray, path: str):
+        s = np.ascontiguousarray(spectrum, dtype=SPECTRUM_CELL).reshape(-1)
+        if self.L.grm_write_spectrum_stats(self.h, _ptr(s), path.encode()) != 0:
+            raise IOError(self.L.grm_model_last_error().decode())
 
 
 class Engine:

@@ -928,6 +928,23 @@ int grm_write_spectrum(const grm_model *m, const grm_spectrum_cell *spec, const 
     return 0;
 }
 
+int grm_write_spectrum_stats(const grm_model *m, const grm_spectrum_cell *spec, const char *path) {
+    if (!m || !spec || !path) return set_err("null argument");
+    FILE *fp = std::fopen(path, "w");
+    if (!fp) return set_err(std::string("Cannot open file ") + path);
+    std::fprintf(fp, "# log10(E/me c^2); per theta bin 0..%d: nph dn_dle de_dle\n", GRM_N_TH_BINS - 1);
+    for (int i = 0; i < GRM_N_E_BINS; ++i) {
+        std::fprintf(fp, "%.17g", (i * SPEC_D_L_E + K.spec_l_e_0) / kLn10);
+        for (int j = 0; j < GRM_N_TH_BINS; ++j) {
+            const grm_spectrum_cell &s = spec[j * GRM_N_E_BINS + i];
+            std::fprintf(fp, " %.17g %.17g %.17g", s.nph, s.dn_dle, s.de_dle);
+        }
+        std::fprintf(fp, "\n");
+    }
+    const bool ok = std::fclose(fp) == 0;
+    return ok ? 0 : set_err(std::string("write failed: ") + path);
+}
+
 int grm_engine_create_from_model(const grm_model *m, int device, grm_engine **out) {
     if (!m || !m->inited) return set_err("model not initialised");
     const double *f[8];

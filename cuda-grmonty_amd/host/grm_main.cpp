@@ -4,7 +4,7 @@
  *
  *   grmonty_amd --harm_dump_path=DUMP --spectrum_path=OUT [--photon_n=5000000]
  *               [--mass_unit=4e19] [--verbosity=info] [--device=0] [--seed=123]
- *               [--batch=67108864] [--threads=0] [--host_emit]
+ *               [--batch=67108864] [--threads=0] [--host_emit] [--stats_path=OUT.stats]
  *
  * read_file -> init -> run_simulation (zone batches emitted and tracked on the GPU; --host_emit:
  * emitted on host threads, batch b+1 overlapping the transport of batch b) -> report_spectrum.
@@ -53,7 +53,7 @@ bool flag(int argc, char **argv, int &i, const char *name, std::string &val) {
 int main(int argc, char **argv) {
     long long photon_n = 5000000; /* main.cpp:20 */
     double mass_unit = 4e19;      /* main.cpp:21 */
-    std::string dump, spec_path, verbosity = "info";
+    std::string dump, spec_path, stats_path, verbosity = "info";
     int device = 0, threads = 0;
     unsigned long long seed = 123; /* consts.hpp:14 */
     long long batch = 1ll << 26; /* photons per zone batch (8.6 GB of emitted photons) */
@@ -65,6 +65,7 @@ int main(int argc, char **argv) {
         else if (flag(argc, argv, i, "harm_dump_path", v)) dump = v;
         else if (flag(argc, argv, i, "spectrum_path", v)) spec_path = v;
         else if (flag(argc, argv, i, "verbosity", v)) verbosity = v;
+        else if (flag(argc, argv, i, "stats_path", v)) stats_path = v;
         else if (flag(argc, argv, i, "device", v)) device = std::atoi(v.c_str());
         else if (flag(argc, argv, i, "seed", v)) seed = std::strtoull(v.c_str(), nullptr, 10);
         else if (flag(argc, argv, i, "batch", v)) batch = std::atoll(v.c_str());
@@ -189,6 +190,10 @@ int main(int argc, char **argv) {
         }
         info("\tlumosity: %g", lm[0]);
         info("\tmax_tau_scatt: %g", lm[1]);
+    }
+    if (!stats_path.empty() && grm_write_spectrum_stats(m, spec.data(), stats_path.c_str())) {
+        std::fprintf(stderr, "[error] %s\n", grm_model_last_error());
+        return 1;
     }
     grm_engine_destroy(e);
     grm_model_free(m);

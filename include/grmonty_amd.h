@@ -264,6 +264,10 @@ int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm
 /* report_spectrum (harm_model.cpp:416-471): 200 rows x 37 columns "%10.5g ".
  * out2 (optional): luminosity, max tau_scatt. */
 int grm_write_spectrum(const grm_model *m, const grm_spectrum_cell *spectrum, const char *path, double out2[2]);
+/* statistics sidecar of the spectrum file (not in the reference): 200 rows of
+ * log10(E) then, per theta bin, nph (recorded superphotons), dn_dle (sum w) and de_dle (sum w E),
+ * "%.17g" -- what an effective-N / KS comparison of two spectra needs and the 37-column file lacks. */
+int grm_write_spectrum_stats(const grm_model *m, const grm_spectrum_cell *spectrum, const char *path);
 
 /* --- per-function device probes (parity tests; one lane per input) --------------------- */
 /* which: see GRM_PROBE_* in DESIGN.md / csrc/grm_probe.hip. in/out are host arrays of

@@ -1874,6 +1874,10 @@ void grmo_reset_spectrum(grmo_model *m) {
     m->n_created = m->n_scatt = m->n_recorded = m->n_steps = 0;
 }
 
+void grmo_set_spectrum(grmo_model *m, const grmo_spectrum in[6 * 200]) {
+    std::memcpy(m->spectrum, in, sizeof(m->spectrum));
+}
+
 void grmo_get_spectrum(const grmo_model *m, grmo_spectrum out[6 * 200]) {
     std::memcpy(out, m->spectrum, sizeof(m->spectrum));
 }
@@ -1967,6 +1971,19 @@ double grmo_run_simulation(grmo_model *m, uint64_t seed) {
     }
     auto t1 = std::chrono::steady_clock::now();
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+/* run_simulation with every photon end written to `trace` (per-photon records for the statistical
+ * parity fixtures, tools/make_golden_192.py); same stream and order as grmo_run_simulation */
+double grmo_run_simulation_traced(grmo_model *m, uint64_t seed, grmo_trace *trace, size_t trace_cap, int64_t *n_trace) {
+    m->trace = trace;
+    m->trace_cap = trace ? trace_cap : 0;
+    m->trace_n = 0;
+    const double t = grmo_run_simulation(m, seed);
+    *n_trace = (int64_t)m->trace_n;
+    m->trace = nullptr;
+    m->trace_cap = 0;
+    return t;
 }
 
 /* harm_model.cpp:416-471, 532-536 */

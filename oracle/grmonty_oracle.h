@@ -171,6 +171,7 @@ int64_t grmo_track_batch(grmo_model *m, const grmo_init_photon *ph, size_t n, in
                          uint64_t id_base, int bias_mode, uint64_t scatt0, uint64_t rec0, double max_tau0,
                          grmo_trace *trace, size_t trace_cap);
 void grmo_reset_spectrum(grmo_model *m);
+void grmo_set_spectrum(grmo_model *m, const grmo_spectrum in[6 * 200]);
 void grmo_get_spectrum(const grmo_model *m, grmo_spectrum out[6 * 200]);
 /* counters: created, scattered, recorded ; plus steps (transport loop iterations) */
 void grmo_get_counters(const grmo_model *m, uint64_t out[4]);
@@ -188,6 +189,8 @@ int64_t grmo_emit_philox(grmo_model *m, uint64_t seed, int64_t z0, int64_t z1, g
 /* ---- whole run, reference CPU semantics (main.cpp:43-53, harm_model.cpp:340-414) ---- */
 /* run_simulation with mt19937(123) shared by emission and transport, live counters. */
 double grmo_run_simulation(grmo_model *m, uint64_t seed); /* returns wall seconds */
+double grmo_run_simulation_traced(grmo_model *m, uint64_t seed, grmo_trace *trace, size_t trace_cap,
+                                  int64_t *n_trace);
 int grmo_report_spectrum(const grmo_model *m, const char *path, double out_lum_maxtau[2]);
 
 size_t grmo_sizeof(int which); /* 0 header 1 units 2 init_photon 3 spectrum 4 fluid 5 trace */

@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("GRMO_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libref_partial.so")
 
 DP = C.POINTER(C.c_double)
@@ -113,11 +113,13 @@ def lib():
                                              C.c_uint64, C.c_uint64, C.c_double, vp, C.c_size_t]),
             "grmo_reset_spectrum": (None, [vp]),
             "grmo_get_spectrum": (None, [vp, vp]),
+            "grmo_set_spectrum": (None, [vp, vp]),
             "grmo_get_counters": (None, [vp, U64P]),
             "grmo_emit": (C.c_int64, [vp, C.c_uint64, vp, C.c_size_t, C.POINTER(C.c_int)]),
             "grmo_init_zone": (None, [vp, C.c_int, C.c_int, DP]),
             "grmo_emit_philox": (C.c_int64, [vp, C.c_uint64, C.c_int64, C.c_int64, vp, C.c_size_t]),
             "grmo_run_simulation": (C.c_double, [vp, C.c_uint64]),
+            "grmo_run_simulation_traced": (C.c_double, [vp, C.c_uint64, vp, C.c_size_t, C.POINTER(C.c_int64)]),
             "grmo_report_spectrum": (C.c_int, [vp, C.c_char_p, DP]),
             "grmo_sizeof": (C.c_size_t, [C.c_int]),
             "grmo_dbg_push_stats": (None, [U64P]),
@@ -257,6 +259,11 @@ class OracleModel:
         self.L.grmo_get_spectrum(self.h, s.ctypes.data_as(C.c_void_p))
         return s.reshape(6, 200)
 
+    def set_spectrum(self, spec: np.ndarray):
+        s = np.ascontiguousarray(spec, dtype=SPECTRUM_CELL).reshape(-1)
+        assert len(s) == 6 * 200
+        self.L.grmo_set_spectrum(self.h, s.ctypes.data_as(C.c_void_p))
+
     def counters(self):
         c = np.zeros(4, dtype=np.uint64)
         self.L.grmo_get_counters(self.h, ptr(c, U64P))
@@ -267,6 +274,13 @@ class OracleModel:
 
     def run_simulation(self, seed: int = 123) -> float:
         return self.L.grmo_run_simulation(self.h, seed)
+
+    def run_simulation_traced(self, seed: int = 123, trace_cap: int = 1 << 23):
+        """run_simulation (reference stream and order) with every photon end recorded"""
+        tr = np.zeros(trace_cap, dtype=TRACE)
+        n = C.c_int64(0)
+        t = self.L.grmo_run_simulation_traced(self.h, seed, tr.ctypes.data_as(C.c_void_p), trace_cap, C.byref(n))
+        return t, tr[:min(n.value, trace_cap)], n.value
 
     def report(self, path: str | None):
         out = np.zeros(2)

@@ -1,0 +1,43 @@
+"""Headline-scale statistical fixtures (tests/golden/oracle_synth192_pn1e5.*, tools/make_golden_192.py):
+six oracle run_simulation runs (reference CPU semantics: serial, mt19937, live adaptive bias) on
+the 192x192 dump019-class synthetic dump at photon_n = 1e5 (BASELINE configs[0]).
+
+These tests calibrate the statistic the GPU parity test (tests/test_gpu_parity_192.py) applies to
+the device: independent reference-semantics runs must pass the binned Kish-N KS test on nu L_nu
+against each other, per theta bin and summed, at the test's own alpha."""
+import json
+import os
+
+import numpy as np
+
+from spectrum_stats import binned_ks, ks_crit
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = os.path.join(HERE, "golden", "oracle_synth192_pn1e5")
+
+
+def test_oracle_seeds_pass_binned_ks():
+    g = np.load(G + ".npz")
+    cells = g["cells"]
+    worst = 0.0
+    for i in range(len(cells)):
+        for j in range(i + 1, len(cells)):
+            for th in [None, 0, 1, 2, 3, 4, 5]:
+                d, n1, n2 = binned_ks(cells[i], cells[j], th)
+                worst = max(worst, d / ks_crit(n1, n2, 1e-3))
+    print(f"worst D / crit(alpha=1e-3) over {len(cells) * (len(cells) - 1) // 2} seed pairs x 7: {worst:.2f}")
+    assert worst < 1.0
+
+
+def test_fixture_consistency():
+    g = np.load(G + ".npz")
+    s = json.load(open(G + ".json"))
+    cnt = g["counters"]  # created, scattered, recorded, steps
+    for k, run in enumerate(s["runs"]):
+        assert run["seed"] == int(g["seeds"][k])
+        assert (run["created"], run["scattered"], run["recorded"], run["steps"]) == tuple(int(x) for x in cnt[k])
+        # every recorded superphoton lands in exactly one cell (record_super_photon, harm_model.cpp:1306-1333)
+        assert int(round(g["cells"][k][:, 0].sum())) == run["recorded"]
+    spec = g["spectrum123"]  # [6, 200, 13]: nph field (index 2) of seed 123
+    assert int(round(spec[:, :, 2].sum())) == s["runs"][0]["recorded"]
+    np.testing.assert_allclose(spec[:, :, 1].reshape(-1), g["cells"][0][:, 3], rtol=1e-9)

@@ -27,19 +27,6 @@ def dump192(dump_dir):
     return write_dump(os.path.join(dump_dir, "synth192.dump"), 192, 192)
 
 
-def _trace_match(tr_o, tr_g):
-    go = {int(r["id"]): r for r in tr_o}
-    gg = {int(r["id"]): r for r in tr_g}
-    match = 0
-    for i in set(go) & set(gg):
-        a, b = go[i], gg[i]
-        if (a["end_reason"] == b["end_reason"] and a["ix2"] == b["ix2"] and a["i_e"] == b["i_e"]
-                and a["n_scatt"] == b["n_scatt"] and abs(a["n_step"] - b["n_step"]) <= 1
-                and np.isclose(a["w"], b["w"], rtol=1e-6, atol=0) and np.isclose(a["e"], b["e"], rtol=1e-9)):
-            match += 1
-    return len(go), len(gg), match
-
-
 def test_grid512_photon_by_photon(dump512):
     import grmonty_amd as G
     import oracle_py as O
@@ -52,6 +39,7 @@ def test_grid512_photon_by_photon(dump512):
     oracle.reset()
     tr_o = oracle.track(sel, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=1000, rec0=2000,
                         max_tau0=model.scalars()["max_tau_scatt"], trace_cap=2_000_000)
+    spec_o = oracle.spectrum()
     eng = G.Engine(model, device=0)
     eng.reset()
     eng.set_option(G.OPT_SEED, 123)
@@ -63,11 +51,15 @@ def test_grid512_photon_by_photon(dump512):
     eng.set_option(G.OPT_TRACE_CAP, 2_000_000)
     eng.track(sel)
     tr_g = eng.trace(2_000_000)
+    spec_g = eng.finish()[0]
     st = eng.stats()
     assert st["n_dropped"] == 0 and st["n_primaries"] == len(sel)
-    n_o, n_g, match = _trace_match(tr_o, tr_g)
-    print(f"512^2: oracle ends {n_o} device ends {n_g} matching {match / n_o:.4f}")
-    assert match / n_o > 0.95
+    from parity_util import MIN_MATCH, check_spectrum_cells, trace_match
+    n_o, n_g, match, bad = trace_match(tr_o, tr_g)
+    n_cmp, n_excl = check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad)
+    print(f"512^2: oracle ends {n_o} device ends {n_g} matching {match / n_o:.4f}; spectrum cells compared "
+          f"(12 fields) {n_cmp}, excluded {n_excl}")
+    assert match / n_o >= MIN_MATCH
 
 
 def test_photon_n_1e7_consistency(dump192):
