@@ -74,14 +74,21 @@ static_assert(sizeof(Cold) == 80, "Cold layout");
 struct DevCounters {
     unsigned long long n_recorded, n_scatt, max_tau_bits, n_steps;
     unsigned long long n_tracked, n_children, n_overflow, n_dropped;
-    unsigned long long n_primaries, max_nstep, n_long, n_abandoned, abort, n_nan, pad[2];
+    unsigned long long n_primaries, max_nstep, n_long, n_abandoned, abort, n_nan;
+    unsigned long long pad[2];
 };
+static_assert(sizeof(DevCounters) == 16 * 8, "DevCounters layout (grm_engine_debug_counters)");
 
 struct Ctl {
     const void *pool;      /* grm_init_photon[] (kind 0) or SReq[] (kind 1) */
     int pool_kind;
     unsigned long long n_pool;
     unsigned long long *pool_head;
+    /* claim order: the head counts claim positions; position q < pos_end holds pool photon
+     * (q mod 2^pool_sh) * pool_m + q / 2^pool_sh (a hole when that is >= n_pool).  Primaries are
+     * interleaved over 2^pool_sh evenly spaced runs of the zone-ordered batch (see run_transport) */
+    unsigned long long pos_end, pool_m;
+    int pool_sh;
     uint64_t id_base;
     uint32_t key0, key1;
     SReq *stack;           /* [lanes][STACK_DEPTH] */
@@ -106,6 +113,7 @@ struct Ctl {
      * in the serial reference (harm_model.cpp:1391-1404).  *admit_end = end of the admitted batch
      * (~0 = no limit), *in_flight = photons started and not ended (children counted when pushed). */
     unsigned long long admit_n, admit_h0, admit_lim;
+    int admit_slack;
     unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     int lanes;
@@ -509,7 +517,7 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const 
  * 2 x 11 x 8 B x 512 lanes = 88 KB (+ 40 KB of lane fields, 16 KB of lane ints): no global memory
  * traffic on the halving path. */
 constexpr int LDS_DOUBLES_PER_LANE = 11;
-constexpr int WARM_GRID = 64; /* workgroups of the warm-up launch (batches of <= lanes/2 photons) */
+constexpr unsigned WARM_BLOCKS = 64; /* workgroups that take the warm-up's admission batches */
 
 __device__ __forceinline__ void save_xkdk(const Slot &s, const Lane &L) {
 #pragma unroll
@@ -894,6 +902,20 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     while (true) {
         ++wave_trips;
         TCOUNT(4);
+        if (warm && blockIdx.x >= WARM_BLOCKS) {
+            /* the warm-up's admission batches are small: the waves of the first WARM_BLOCKS
+             * workgroups take them, the rest wait here without touching the counters (their polling
+             * would contend with the warm-up's own counter traffic) until the admission is over */
+            unsigned long long end = 0;
+            if (lane_id == 0) end = __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane((int)(end >> 32)) != -1 ||
+                __builtin_amdgcn_readfirstlane((int)end) != -1) {
+                __builtin_amdgcn_s_sleep(127);
+                continue;
+            }
+            warm = false;
+            if (!C.bias_frozen) bias_d = bias_den(P, C);
+        }
         if ((trip++ & (REFRESH_TRIPS - 1)) == 0 || warm) {
             flush_counters(C);
             if (!C.bias_frozen) bias_d = bias_den(P, C);
@@ -904,6 +926,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                     if (lane_id == 0) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if (stop) { /* abandon: drop the lane photons, the wave's stack and the pool; exit */
+                    /* end the admission too, so that waves parked for it wake up and exit */
+                    if (lane_id == 0) __hip_atomic_store(C.admit_end, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (active) {
                         record_stuck(C, L);
                         atomicAdd(&C.ctr->n_abandoned, 1ull);
@@ -965,8 +989,11 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                         got = (long long)want;
                                     else
                                         atomicAdd(C.in_flight, (unsigned long long)(-(long long)want));
-                                } else if (__hip_atomic_load(C.in_flight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                                           0) {
+                                } else if (__hip_atomic_load(C.in_flight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <=
+                                           ((C.admit_h0 + end) >> C.admit_slack)) {
+                                    /* the next batch once all but a straggler fraction of the history
+                                     * has ended: the counters then hold nearly all of it, and one
+                                     * long-lived photon does not hold the warm-up up */
                                     const unsigned long long h = C.admit_h0 + end;
                                     const unsigned long long next =
                                         end >= C.admit_n ? ~0ull
@@ -983,11 +1010,11 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                             base = __shfl(base, 0);
                             k_pool = (int)__shfl(got, 0);
                         }
-                        if (k_pool > 0 && base + k_pool >= C.n_pool) pool_done = true;
+                        if (k_pool > 0 && base + k_pool >= C.pos_end) pool_done = true;
                     } else {
                         if (lane_id == 0) base = atomicAdd(C.pool_head, (unsigned long long)k_pool);
                         base = __shfl(base, 0);
-                        if (base + k_pool >= C.n_pool) pool_done = true;
+                        if (base + k_pool >= C.pos_end) pool_done = true;
                     }
                 }
                 if (lane_id == 0) *wtop = top - k_child;
@@ -1006,8 +1033,11 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 }
                 TSTAMP(0);
                 if (!active && r >= k_child && r - k_child < k_pool) {
-                    const unsigned long long idx = base + (unsigned long long)(r - k_child);
-                    if (idx < C.n_pool) {
+                    const unsigned long long pos = base + (unsigned long long)(r - k_child);
+                    const unsigned long long idx =
+                        (pos & ((1ull << C.pool_sh) - 1)) * C.pool_m + (pos >> C.pool_sh);
+                    if (pos < C.pos_end && idx >= C.n_pool) --L.flight(); /* a hole: claimed, ends at once */
+                    if (pos < C.pos_end && idx < C.n_pool) {
                         if (C.pool_kind == 0) {
                             load_primary(C, idx, L, cold);
                             ++L.c_primaries();
@@ -1162,7 +1192,8 @@ struct grm_engine {
     int grid_override = 0;
     double max_tau_init = 0.0;
     bool frozen_set = false;
-    int64_t warmup = -1;     /* photons; -1 = lanes */
+    int64_t warmup = 32768;  /* photons; -1 = lanes */
+    int warmup_slack = 4;
     int refill_min = 2;      /* primaries: set-up is in the trip (phase 3), so refill early */
     int child_min = 8;       /* children: batch the divergent scattering sampling */
     uint64_t history = 0;    /* primaries tracked since reset */
@@ -1266,14 +1297,20 @@ int ensure_ovf(grm_engine *e, unsigned long long cap) {
     return 0;
 }
 
-int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid) {
-    if (n == 0) return 0;
+/* one launch (+ overflow relaunches) over claim positions [pos0, pos1) of a batch of n primaries
+ * interleaved as 2^sh runs of m (Ctl.pos_end) */
+int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, uint64_t m, uint64_t pos0,
+               uint64_t pos1, int grid) {
+    if (pos1 <= pos0) return 0;
     /* overflow pool: children rarely spill (8-deep lane stacks); size ~ max(1M, n/4) */
-    if (ensure_ovf(e, std::max<unsigned long long>(1ull << 20, n / 4))) return -1;
+    if (ensure_ovf(e, std::max<unsigned long long>(1ull << 20, (pos1 - pos0) / 4))) return -1;
     Ctl C{};
     C.pool = d_batch;
     C.pool_kind = 0;
     C.n_pool = n;
+    C.pos_end = pos1;
+    C.pool_m = m;
+    C.pool_sh = sh;
     C.pool_head = e->d_small + 0;
     C.id_base = e->id_base;
     C.key0 = (uint32_t)e->seed;
@@ -1302,9 +1339,10 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
         const uint64_t limit = e->warmup < 0 ? (uint64_t)e->lanes : (uint64_t)e->warmup;
-        C.admit_n = (!e->bias_mode && e->history < limit) ? std::min<uint64_t>(n, limit - e->history) : 0;
+        C.admit_n = (!e->bias_mode && e->history < limit && pos0 == 0) ? std::min<uint64_t>(pos1, limit - e->history) : 0;
         C.admit_h0 = e->history;
         C.admit_lim = limit;
+        C.admit_slack = e->warmup_slack;
     }
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
@@ -1328,9 +1366,14 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     double ms_total = 0.0;
     unsigned long long steps_pass = steps_before;
     int src = -1, dst = 0;
-    unsigned long long n_pool = n;
+    unsigned long long n_pool = pos1 - pos0;
     for (int pass = 0; n_pool > 0; ++pass) {
         if (zero_async(e, e->d_small, 3 * sizeof(unsigned long long))) return -1;
+        if (pass == 0 && pos0) { /* [0] pool head = first claim position */
+            e->pin->word[1] = pos0;
+            HIPCHK(e, hipMemcpyAsync(e->d_small, &e->pin->word[1], sizeof(unsigned long long), hipMemcpyHostToDevice,
+                                     e->stream));
+        }
         if (pass == 0 && C.admit_n) { /* [4] in flight = 0, [5] end of the first warm-up batch */
             const unsigned long long h = C.admit_h0;
             e->pin->word[2] = 0;
@@ -1347,6 +1390,9 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
             C.pool = e->d_ovf[src];
             C.pool_kind = 1;
             C.n_pool = n_pool;
+            C.pos_end = n_pool;
+            C.pool_m = n_pool;
+            C.pool_sh = 0;
             C.admit_n = 0;
         }
         if (zero_async(e, &e->d_ctr->abort, sizeof(unsigned long long))) return -1;
@@ -1396,31 +1442,41 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int grid
     e->stats.kernel_ms += ms_total;
     e->stats.last_kernel_ms += ms_total;
     e->stats.last_steps += h.n_steps - steps_before;
-    e->id_base += n;
-    e->history += n;
+    e->history += pos1 - pos0;
     return 0;
 }
 
-/* one transport call = one persistent launch (+ overflow relaunches); the live-bias warm-up is
- * admission control inside the launch (Ctl.admit_n) */
+/* One transport call = one persistent launch (+ overflow relaunches); the live-bias warm-up is
+ * admission control inside the launch (Ctl.admit_n).
+ *
+ * Claim order.  The batch is in zone-walk order (emission, harm_model.cpp:673-704), and the
+ * adaptive bias (bias_func, :1391-1404) is driven by the counters of RECORDED photons.  The inner
+ * zones' photons fall into the hole and never record, so a zone-ordered claim sequence would start
+ * ~lanes photons of the zones where escape begins all at once on the bias of an empty history --
+ * where the serial reference adapts after the first few records -- and their scattering cascades
+ * would inflate the recorded / scattered counts ~2x (measured: 5.1 M vs the reference's 2.3 M at
+ * 192^2, photon_n = 1e5).  Claims therefore interleave 2^CLAIM_SH evenly spaced runs of the batch:
+ * claim position q takes photon (q mod 2^CLAIM_SH) * m + q / 2^CLAIM_SH, so every admission batch
+ * and every stretch of the bulk samples the whole zone range, records start at once and the
+ * counters evolve as in the serial run (photon ids, and so the Philox streams, stay the batch
+ * index: results depend on the order only through the bias). */
+constexpr int CLAIM_SH = 12;
+
 int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     if (alloc_lanes(e)) return -1;
     e->stats.last_kernel_ms = 0.0;
     e->stats.last_steps = 0;
     e->stats.max_launch_ms = 0.0;
     e->stats.max_launch_steps = 0;
-    /* the live-bias warm-up (admission batches, mostly idle lanes waiting for a batch to finish) runs
-     * as its own launch on a small grid, so its CUs stay free for other work on the device (e.g. the
-     * next pass's engine); then the rest on the full grid */
-    const uint64_t limit = e->warmup < 0 ? (uint64_t)e->lanes : (uint64_t)e->warmup;
-    if (!e->bias_mode && e->history < limit && n > 0) {
-        const size_t w = (size_t)std::min<uint64_t>(n, limit - e->history);
-        const int grid_w = std::min(e->grid, WARM_GRID);
-        if (run_passes(e, d_batch, w, grid_w)) return -1;
-        d_batch += w;
-        n -= w;
-    }
-    return run_passes(e, d_batch, n, e->grid);
+    if (n == 0) return 0;
+    const int sh = n >= (2ull << CLAIM_SH) ? CLAIM_SH : 0;
+    const uint64_t m = (n + (1ull << sh) - 1) >> sh, n_pos = m << sh;
+    /* one launch on the full grid: the live-bias warm-up (the first positions in admission batches)
+     * is admission control inside it, and the claims run free as soon as it is over, while the
+     * warm-up's own long-lived photons are still in flight */
+    if (run_passes(e, d_batch, n, sh, m, 0, n_pos, e->grid)) return -1;
+    e->id_base += n;
+    return 0;
 }
 
 int reset_counters(grm_engine *e) {
@@ -1584,6 +1640,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_WARMUP: e->warmup = v; return 0;
     case GRM_OPT_REFILL_MIN: e->refill_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_CHILD_MIN: e->child_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
+    case GRM_OPT_WARMUP_SLACK: e->warmup_slack = v < 0 ? 0 : (v > 30 ? 30 : (int)v); return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }
@@ -1772,6 +1829,15 @@ int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap) {
     if (k && out && hipMemcpy(out, e->d_waves, k * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return (int64_t)n;
+}
+
+int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]) {
+    if (!e || !out) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    DevCounters h;
+    if (read_counters(e, h)) return -1;
+    std::memcpy(out, &h, sizeof(h));
+    return 0;
 }
 
 int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap) {

@@ -47,6 +47,7 @@ OPT_SEED, OPT_BIAS_MODE, OPT_TRACE_CAP, OPT_GRID_BLOCKS, OPT_ID_BASE = 0, 1, 2, 
 OPT_FROZEN_SCATT, OPT_FROZEN_REC, OPT_FROZEN_MAXTAU, OPT_WARMUP, OPT_REFILL_MIN = 5, 6, 7, 8, 9
 OPT_WATCHDOG_MS = 10
 OPT_CHILD_MIN = 11
+OPT_WARMUP_SLACK = 12
 N_TH_BINS, N_E_BINS = 6, 200
 
 
@@ -118,6 +119,7 @@ SIGNATURES = {
     "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
     "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_stuck": (C.c_int64, [VP, VP, C.c_size_t]),
+    "grm_engine_debug_counters": (C.c_int, [VP, C.POINTER(C.c_uint64)]),
     "grm_sizeof": (C.c_size_t, [C.c_int]),
     "grm_version": (C.c_char_p, []),
 }
@@ -366,6 +368,16 @@ class Engine:
         if n < 0:
             raise RuntimeError(self.L.grm_engine_last_error(self.h).decode())
         return out[:n]
+
+    def debug_counters(self) -> dict:
+        """raw device counters (grm_engine_debug_counters)"""
+        out = (C.c_uint64 * 16)()
+        self._check(self.L.grm_engine_debug_counters(self.h, out))
+        v = list(out)
+        f = lambda b: float(np.array([b], dtype=np.uint64).view(np.float64)[0])  # noqa: E731
+        return {"n_recorded": v[0], "n_scatt": v[1], "max_tau_scatt": f(v[2]), "n_steps": v[3],
+                "n_tracked": v[4], "n_children": v[5], "n_overflow": v[6], "n_dropped": v[7], "n_primaries": v[8],
+                "max_photon_steps": v[9], "n_long": v[10], "n_abandoned": v[11], "n_nan": v[13]}
 
     def allreduce(self):
         self._check(self.L.grm_engine_allreduce(self.h))

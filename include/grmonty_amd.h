@@ -132,9 +132,11 @@ enum {
     GRM_OPT_FROZEN_SCATT = 5,  /* N_scatt */
     GRM_OPT_FROZEN_REC = 6,    /* N_recorded */
     GRM_OPT_FROZEN_MAXTAU = 7, /* max tau_scatt, IEEE-754 bit pattern of the double */
-    /* live-bias warm-up: until this many photons have been tracked since the last reset, a
-     * batch is cut into launches that double the history each time, so the adaptive bias
-     * counters evolve as in the serial reference (-1 = one persistent grid's worth of lanes, 0 = off) */
+    /* live-bias warm-up: until this many photons have been claimed since the last reset, they are
+     * admitted in batches that double the history each time (the next batch once all but a
+     * 2^-GRM_OPT_WARMUP_SLACK fraction of the history has ended), so the adaptive-bias counters
+     * evolve as in the serial reference (default 32768; -1 = one persistent grid's worth of lanes;
+     * 0 = off).  Tuned by the reference-semantics counters at 192^2 */
     GRM_OPT_WARMUP = 8,
     /* idle lanes a wavefront gathers before it takes emitted photons (1..64, default 2) */
     GRM_OPT_REFILL_MIN = 9,
@@ -145,7 +147,9 @@ enum {
     GRM_OPT_WATCHDOG_MS = 10,
     /* scattered children a wavefront samples together (1..64, default 8): larger = less divergent
      * scattering sampling, more idle lane-trips while a batch gathers */
-    GRM_OPT_CHILD_MIN = 11
+    GRM_OPT_CHILD_MIN = 11,
+    /* warm-up straggler tolerance, log2 (default 4: 1/16 of the history may still be in flight) */
+    GRM_OPT_WARMUP_SLACK = 12
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
@@ -191,6 +195,10 @@ int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap);
 /* diagnostic: state of the photons the watchdog abandoned, 16 doubles each: id, n_step, phase, depth,
  * pend, w, e_0_s, dl, x[4], k[4].  out holds cap records; returns the records kept (<= 256). */
 int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap);
+/* raw device counters: n_recorded, n_scatt, max_tau_scatt bits, n_steps, n_tracked, n_children,
+ * n_overflow, n_dropped, n_primaries, max photon steps, lives > 1e5 steps, n_abandoned, abort, n_nan,
+ * 2 reserved */
+int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]);
 
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
 /* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */

@@ -13,6 +13,8 @@ import numpy as np
 MIN_MATCH = 0.99       # observed: 1.0000 (r01/r02 GPU logs); a flip is a last-bit event
 W_RTOL, E_RTOL = 1e-6, 1e-9
 SPEC_RTOL = 1e-6       # per-cell sums of matching photons: the weight tolerance
+SPEC_ATOL = 1e-12      # x the field's total: underflow-level terms (e.g. an absorption optical depth of
+                       # 1e-263 that one side's exp rounds to 0) are not a disagreement
 SPEC_FIELDS = ["dn_dle", "de_dle", "nph", "nscatt", "x1i_av", "x2i_sq", "x3f_sq", "tau_abs", "tau_scatt",
                "ne_0", "theta_e_0", "b_0"]
 
@@ -44,6 +46,7 @@ def check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad):
     so = np.asarray(spec_o).reshape(6, 200)
     sg = np.asarray(spec_g).reshape(6, 200)
     n_cmp = 0
+    floor = {f: SPEC_ATOL * max(np.abs(so[f]).sum(), np.abs(sg[f]).sum()) for f in SPEC_FIELDS}
     for j in range(6):
         for i in range(200):
             if (j, i) in excl:
@@ -51,5 +54,5 @@ def check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad):
             n_cmp += 1
             for f in SPEC_FIELDS:
                 a, b = float(so[f][j, i]), float(sg[f][j, i])
-                assert abs(a - b) <= SPEC_RTOL * max(abs(a), abs(b)), (f, j, i, a, b)
+                assert abs(a - b) <= SPEC_RTOL * max(abs(a), abs(b)) + floor[f], (f, j, i, a, b)
     return n_cmp, len(excl)

@@ -1,0 +1,3 @@
+#!/bin/bash
+R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R" && mkdir -p gpurun_out
+SEEDS=123,124,125,126,127,128 timeout -k 10 500 python -u tools/bias_probe.py "$@" > gpurun_out/bias_probe.log 2>&1; rc=$?; cat gpurun_out/bias_probe.log; exit $rc
