@@ -79,6 +79,7 @@ struct DevCounters {
 };
 static_assert(sizeof(DevCounters) == 16 * 8, "DevCounters layout (grm_engine_debug_counters)");
 
+struct LoneRec;
 struct Ctl {
     const void *pool;      /* grm_init_photon[] (kind 0) or SReq[] (kind 1) */
     int pool_kind;
@@ -123,6 +124,11 @@ struct Ctl {
     unsigned long long watchdog_ticks;
     double *stuck;
     unsigned long long stuck_cap, *stuck_count;
+    /* lone photons handed over to lone_kernel (null = never); lone_all: every photon is handed over
+     * at the top of its first step (GRM_OPT_LONE = 2: tests of the lone path) */
+    LoneRec *lone;
+    unsigned long long lone_cap, *lone_count;
+    int lone_all;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -229,27 +235,29 @@ __device__ __forceinline__ void tstamp(int r) {
 #endif
 
 /* stop_criterion (harm_model.cpp:1589-1616) */
-__device__ __forceinline__ bool stop_criterion(const Params &P, Lane &L) {
-    if (L.x[1] < P.x1_min) return true;
-    if (L.x[1] > P.x1_max) {
-        if (L.w < WEIGHT_MIN) {
-            if (uniform(L.rng) <= 1.0 / ROULETTE)
-                L.w *= ROULETTE;
+__device__ __forceinline__ bool stop_criterion(const Params &P, double x1, double &w, Rng &rng) {
+    if (x1 < P.x1_min) return true;
+    if (x1 > P.x1_max) {
+        if (w < WEIGHT_MIN) {
+            if (uniform(rng) <= 1.0 / ROULETTE)
+                w *= ROULETTE;
             else
-                L.w = 0.0;
+                w = 0.0;
         }
         return true;
     }
-    if (L.w < WEIGHT_MIN) {
-        if (uniform(L.rng) <= 1.0 / ROULETTE) {
-            L.w *= ROULETTE;
+    if (w < WEIGHT_MIN) {
+        if (uniform(rng) <= 1.0 / ROULETTE) {
+            w *= ROULETTE;
         } else {
-            L.w = 0.0;
+            w = 0.0;
             return true;
         }
     }
     return false;
 }
+
+__device__ __forceinline__ bool stop_criterion(const Params &P, Lane &L) { return stop_criterion(P, L.x[1], L.w, L.rng); }
 
 __device__ void write_trace(const Ctl &C, const Cold *cold, uint64_t id, double w, double x1, double x2,
                                          double x3, double tau_abs, double tau_scatt, int n_scatt, int n_step,
@@ -310,7 +318,8 @@ __device__ __forceinline__ void flush_counters(const Ctl &C) {
 
 /* record_super_photon (harm_model.cpp:1291-1335) */
 __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, uint64_t id, double w, double x1,
-                              double x2, double x3, double tau_abs, double tau_scatt, int n_scatt, int n_step) {
+                              double x2, double x3, double tau_abs, double tau_scatt, int n_scatt, int n_step,
+                              double *spec, int cell_stride) {
     int ix2 = -1, i_e = -1, reason = 1;
     const double e = cold->e;
     if (!(isnan(w) || isnan(e))) {
@@ -326,7 +335,7 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
                 reason = 0;
                 atomicAdd(cnt + 0, 1ull);
                 atomicAdd(cnt + 1, (unsigned long long)n_scatt);
-                double *s = spec_slice(C) + (ix2 * N_E_BINS + i_e) * SPEC_FIELDS;
+                double *s = spec + (ix2 * N_E_BINS + i_e) * cell_stride;
                 const double x1i = cold->x1i, x2i = cold->x2i;
                 atomicAdd(s + 0, w);                      /* dn_dle */
                 atomicAdd(s + 1, w * e);                  /* de_dle */
@@ -354,7 +363,8 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
 __device__ __forceinline__ void end_of_life(const Params &P, const Ctl &C, const Cold *cold, const Lane &L) {
     /* record_criterion (harm_model.cpp:1618) && n_step <= max_n_step (:1066) */
     if (L.x[1] > P.x1_max && L.n_step <= MAX_N_STEP)
-        record_photon(P, C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt(), L.n_step);
+        record_photon(P, C, cold, L.rng.id, L.w, L.x[1], L.x[2], L.x[3], L.tau_abs(), L.tau_scatt(), L.n_scatt(), L.n_step,
+                      spec_slice(C), SPEC_FIELDS);
     else
         trace_end(C, cold, L, 2);
 }
@@ -472,15 +482,15 @@ __device__ __forceinline__ void store_sreq(SReq *dst, const SReq &R) {
 
 /* push the scattered photon's child out as a scatter request: onto the wave's stack (HBM entries,
  * top counter in LDS), else the overflow pool (tracked by the next launch).  true = on the stack */
-__device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const Cold *cold, const Fluid &F, double wc,
-                                             SReq *wstack, int *wtop) {
-    SReq R;
+/* the scatter request of a scattered photon's child (scatter_super_photon's inputs, :1071-1145) */
+__device__ __forceinline__ void make_sreq(SReq &R, const double x[4], const double k[4], const Rng &rng, int n_scatt,
+                                          const Cold *cold, const Fluid &F, double wc) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         /* x^0 (Boyer-Lindquist time) enters no result -- not the metric (stationary), the fluid, the
          * record or any test -- so the device does not carry it: children start at x^0 = 0 */
-        R.x[i] = i == 0 ? 0.0 : L.x[i];
-        R.k[i] = L.k[i];
+        R.x[i] = i == 0 ? 0.0 : x[i];
+        R.k[i] = k[i];
         R.u_con[i] = F.u_con[i];
         R.b_con[i] = F.b_con[i];
     }
@@ -490,24 +500,37 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const 
     R.n_e_0 = cold->n_e_0;
     R.theta_e_0 = cold->theta_e_0;
     R.e_0 = cold->e_0;
-    R.id = child_id(L.rng.id, L.rng.ctr);
-    R.parent = L.rng.id;
-    R.n_scatt = L.n_scatt() + 1;
+    R.id = child_id(rng.id, rng.ctr);
+    R.parent = rng.id;
+    R.n_scatt = n_scatt + 1;
     R.pad0 = 0;
     R.pad1 = 0.0;
+}
+
+/* append to the overflow pool (tracked by the next launch) */
+__device__ __forceinline__ void push_overflow_req(const Ctl &C, const SReq &R) {
+    const unsigned long long o = atomicAdd(C.ovf_count, 1ull);
+    if (o < C.ovf_cap)
+        store_sreq(C.ovf + o, R);
+    else
+        atomicAdd(&C.ctr->n_dropped, 1ull);
+    atomicAdd(&C.ctr->n_overflow, 1ull);
+}
+
+/* push the scattered photon's child out as a scatter request: onto the wave's stack (HBM entries,
+ * top counter in LDS), else the overflow pool (tracked by the next launch).  true = on the stack */
+__device__ __forceinline__ bool push_request(const Ctl &C, const double x[4], const double k[4], const Rng &rng,
+                                             int n_scatt, const Cold *cold, const Fluid &F, double wc, SReq *wstack,
+                                             int *wtop) {
+    SReq R;
+    make_sreq(R, x, k, rng, n_scatt, cold, F, wc);
     const int slot = atomicAdd(wtop, 1); /* LDS; values past the cap are clamped at the next refill */
     if (slot < WSTACK_CAP) {
         store_sreq(wstack + slot, R);
         return true;
-    } else {
-        const unsigned long long o = atomicAdd(C.ovf_count, 1ull);
-        if (o < C.ovf_cap)
-            store_sreq(C.ovf + o, R);
-        else
-            atomicAdd(&C.ctr->n_dropped, 1ull);
-        atomicAdd(&C.ctr->n_overflow, 1ull);
-        return false;
     }
+    push_overflow_req(C, R);
+    return false;
 }
 
 /* Two per-lane state copies live in LDS ([slot][lane], conflict-free 8-B words), 11 slots each:
@@ -518,6 +541,7 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const Lane &L, const 
  * traffic on the halving path. */
 constexpr int LDS_DOUBLES_PER_LANE = 11;
 constexpr unsigned WARM_BLOCKS = 64; /* workgroups that take the warm-up's admission batches */
+constexpr unsigned long long RES_CHUNK = 64; /* claim positions a wave reserves per pool-head atomic */
 
 __device__ __forceinline__ void save_xkdk(const Slot &s, const Lane &L) {
 #pragma unroll
@@ -608,30 +632,22 @@ __device__ __forceinline__ double bcast(double v, int src) {
  * step (255 attempts for 128 sub-steps) -- the last photons of a pass -- run ~2x faster.
  * Called by the whole wave (converged); `owner` is wave-uniform.  Every lane's copy of the push
  * state (x, k, dk/dlambda, e_0_s, hlen, depth, pend) follows the owner's; only the owner's is used. */
-__device__ __forceinline__ void halving_walk(const Params &P, Lane &L, int owner) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int rank = lane == owner ? 0 : (lane < owner ? lane + 1 : lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        L.x[i] = bcast(L.x[i], owner);
-        L.k[i] = bcast(L.k[i], owner);
-        L.dk[i] = bcast(L.dk[i], owner);
-    }
-    L.e_0_s = bcast(L.e_0_s, owner);
-    L.hlen = bcast(L.hlen, owner);
-    L.depth = __builtin_amdgcn_readlane(L.depth, owner);
-    L.pend = (uint32_t)__builtin_amdgcn_readlane((int)L.pend, owner);
+/* The halving walk proper, on a push state every lane of the wave holds identically (x, k, dk/dlambda,
+ * e_0_s; the node `depth` of the halving tree being pushed, the pending second halves `pend`); lane
+ * rank r (0 for the state's owner) attempts depth + r.  Leaves the completed push in every lane. */
+__device__ __forceinline__ void walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
+                                          double hlen, int depth, uint32_t pend, int rank, int owner) {
     while (true) {
-        if (!(L.x[1] < P.xs1)) {
+        if (!(x[1] < P.xs1)) {
             /* every lane attempts in place from the same start state; the winner's result is then
              * broadcast over all of them */
-            const int d = L.depth + rank;
+            const int d = depth + rank;
             double e_1 = 0.0;
             bool ok = false;
             if (d <= MAX_SUBDIV) {
                 Trig T;
                 Gcov G;
-                const bool fail = push_attempt(P, L.x, L.k, L.dk, L.e_0_s, ldexp(L.hlen, -d), e_1, T, G);
+                const bool fail = push_attempt(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G);
                 ok = !fail || d == MAX_SUBDIV;
             }
             /* the owner's attempt if it passed, else the shallowest passing helper (helper depth grows
@@ -641,17 +657,303 @@ __device__ __forceinline__ void halving_walk(const Params &P, Lane &L, int owner
             const int dw = __builtin_amdgcn_readlane(d, w);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                L.x[i] = bcast(L.x[i], w);
-                L.k[i] = bcast(L.k[i], w);
-                L.dk[i] = bcast(L.dk[i], w);
+                x[i] = bcast(x[i], w);
+                k[i] = bcast(k[i], w);
+                dk[i] = bcast(dk[i], w);
             }
-            L.e_0_s = bcast(e_1, w);
-            L.pend |= ((2u << dw) - 1u) & ~((2u << L.depth) - 1u); /* second halves at depths depth+1..dw */
-            L.depth = dw;
+            e_0_s = bcast(e_1, w);
+            pend |= ((2u << dw) - 1u) & ~((2u << depth) - 1u); /* second halves at depths depth+1..dw */
+            depth = dw;
         }
-        if (L.pend == 0) break;
-        L.depth = 31 - __builtin_clz(L.pend);
-        L.pend &= ~(1u << L.depth);
+        if (pend == 0) break;
+        depth = 31 - __builtin_clz(pend);
+        pend &= ~(1u << depth);
+    }
+}
+
+__device__ __forceinline__ int walk_rank(int owner) {
+    const int lane = (int)(threadIdx.x & 63);
+    return lane == owner ? 0 : (lane < owner ? lane + 1 : lane);
+}
+
+/* complete the owner's push in progress (phase 1 or 2, any node of its halving tree) with the wave */
+__device__ __forceinline__ void halving_walk(const Params &P, Lane &L, int owner) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        L.x[i] = bcast(L.x[i], owner);
+        L.k[i] = bcast(L.k[i], owner);
+        L.dk[i] = bcast(L.dk[i], owner);
+    }
+    L.e_0_s = bcast(L.e_0_s, owner);
+    const double hlen = bcast(L.hlen, owner);
+    const int depth = __builtin_amdgcn_readlane(L.depth, owner);
+    const uint32_t pend = (uint32_t)__builtin_amdgcn_readlane((int)L.pend, owner);
+    walk_push(P, L.x, L.k, L.dk, L.e_0_s, hlen, depth, pend, walk_rank(owner), owner);
+    L.depth = 0;
+    L.pend = 0;
+}
+
+/* Lone photons.  When a wave's only work left is one photon (the pool is drained, its stack empty),
+ * that photon's latency is the pass's tail: such photons run for 1e5-1e6 steps (trapped
+ * near-circular orbits, polar Zeno stepping, full-depth halving -- all exact reference semantics,
+ * which end them only at max_n_step, harm_model.cpp:1058-1063).  The lane loop is the wrong place
+ * for them (one lane of 64 busy, per-trip refill logic, lane fields in LDS): the wave hands the
+ * photon over (export_lone, at the top of a step) and exits, and after the launch lone_kernel runs
+ * every handed-over photon with a whole wave of its own: straight-line steps of
+ * track_super_photon's loop (:919-1063) with the state in registers, every lane holding the same
+ * values, the pushes as halving walks over the lanes (walk_push), only lane 0 writing.  Its
+ * scattered children go to the overflow pool, which the host relaunches the lane loop over. */
+struct alignas(16) LoneRec {
+    double x[4], k[4], dk[4];
+    double w, e_0_s;
+    double tau_abs, tau_scatt, a_si, a_ai, bi, fl_ne;
+    Cold c;
+    uint64_t id;
+    uint32_t ctr;
+    int32_t n_step, n_scatt, pad;
+};
+static_assert(sizeof(LoneRec) == 272, "LoneRec layout");
+
+__device__ __forceinline__ void export_lone(LoneRec *r, const Lane &L, const Cold *cold) {
+    LoneRec R;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        R.x[i] = L.x[i];
+        R.k[i] = L.k[i];
+        R.dk[i] = L.dk[i];
+    }
+    R.w = L.w;
+    R.e_0_s = L.e_0_s;
+    R.tau_abs = L.tau_abs();
+    R.tau_scatt = L.tau_scatt();
+    R.a_si = L.alpha_scatti();
+    R.a_ai = L.alpha_absi();
+    R.bi = L.bi();
+    R.fl_ne = L.fl_ne();
+    R.c = *cold;
+    R.id = L.rng.id;
+    R.ctr = L.rng.ctr;
+    R.n_step = L.n_step;
+    R.n_scatt = L.n_scatt();
+    R.pad = 0;
+    const double2 *s = reinterpret_cast<const double2 *>(&R);
+    double2 *d = reinterpret_cast<double2 *>(r);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(LoneRec) / 16); ++q) d[q] = s[q];
+}
+
+/* the child of a lone photon's scattering, straight to the overflow pool */
+__device__ __forceinline__ void push_overflow(const Ctl &C, const double x[4], const double k[4], const Rng &rng,
+                                              int n_scatt, const Cold *cold, const Fluid &F, double wc) {
+    SReq R;
+    make_sreq(R, x, k, rng, n_scatt, cold, F, wc);
+    push_overflow_req(C, R);
+}
+
+/* one wave (64-thread block) per handed-over photon */
+__global__ __launch_bounds__(64) void lone_kernel(Params P, Ctl C, unsigned long long n) {
+    if (blockIdx.x >= n) return;
+    const int lane = (int)threadIdx.x;
+    const bool own = lane == 0;
+    const int rank = lane;
+    if (lane < 4) s_cnt[0][lane] = 0;
+    __syncthreads();
+    const LoneRec &R = C.lone[blockIdx.x];
+    double x[4], k[4], dk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[i] = R.x[i];
+        k[i] = R.k[i];
+        dk[i] = R.dk[i];
+    }
+    double w = R.w, e_0_s = R.e_0_s;
+    double tau_abs = R.tau_abs, tau_scatt = R.tau_scatt, a_si = R.a_si, a_ai = R.a_ai, bi = R.bi, fl_ne = R.fl_ne;
+    const Cold *cold = &R.c;
+    int n_step = R.n_step;
+    const int n_scatt = R.n_scatt;
+    Rng rng;
+    rng.k0 = C.key0;
+    rng.k1 = C.key1;
+    rng.id = R.id;
+    rng.ctr = R.ctr;
+    rng.ctr_hi = 0;
+    double bias_d = bias_den(P, C);
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long steps = 0, children = 0;
+    bool ended = false, abandoned = false;
+    int reason = -1; /* ended without a record: trace reason */
+    for (unsigned s = 1;; ++s) {
+        if ((s & (REFRESH_TRIPS - 1)) == 0) {
+            flush_counters(C);
+            if (!C.bias_frozen) bias_d = bias_den(P, C);
+            if (C.watchdog_ticks) {
+                bool stop = __hip_atomic_load(&C.ctr->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (!stop && __builtin_amdgcn_s_memrealtime() - rt_start > C.watchdog_ticks) {
+                    stop = true;
+                    if (own) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (stop) {
+                    abandoned = true;
+                    break;
+                }
+            }
+        }
+        /* while (!stop_criterion(photon)) (:919) */
+        if (stop_criterion(P, x[1], w, rng)) {
+            ended = true;
+            break;
+        }
+        /* photon_2 (:920-925), step size, push (:927-930) */
+        double x2[4], k2[4], dk2[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            x2[i] = x[i];
+            k2[i] = k[i];
+            dk2[i] = dk[i];
+        }
+        const double e0s2 = e_0_s;
+        const double dl = step_size(P, x, k);
+        walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, rank, 0);
+        ++steps;
+        if (stop_criterion(P, x[1], w, rng)) { /* :932-934 */
+            ended = true;
+            break;
+        }
+        if (isnan(x[1])) { /* a NaN position is absorbing (see transport_trip) */
+            if (own) atomicAdd(&C.ctr->n_nan, 1ull);
+            ended = true;
+            reason = 3;
+            break;
+        }
+        if (a_ai > 0.0 || a_si > 0.0 || fl_ne > 0.0) { /* :937 */
+            Trig T;
+            Gcov G;
+            ZoneFetch Z;
+            zone_fetch(P, x, Z); /* issued first: its latency overlaps the metric */
+            trig_at(P, x, T);
+            gcov_from_trig(P, T, G);
+            Fluid F;
+            fluid_from(P, x, G, Z, F);
+            fl_ne = F.n_e;
+            const double nu = fluid_nu(k, F);
+            const bool zero = nu < 0.0 || F.n_e == 0.0; /* bound_flag (:941-955) or nu < 0 */
+            double a_s = 0.0, a_a = 0.0;
+            if (!zero) radiation_coeffs(P, k, F, nu, a_s, a_a);
+            const double bf = zero ? 0.0 : bias_func(bias_d, F.theta_e, w);
+            double d_tau_scatt, d_tau_abs, bias;
+            if (zero) {
+                d_tau_scatt = 0.5 * a_si * P.d_tau_k * dl;
+                d_tau_abs = 0.5 * a_ai * P.d_tau_k * dl;
+                bias = 0.0;
+            } else {
+                d_tau_scatt = 0.5 * (a_si + a_s) * P.d_tau_k * dl;
+                d_tau_abs = 0.5 * (a_ai + a_a) * P.d_tau_k * dl;
+                bias = 0.5 * (bi + bf);
+            }
+            a_si = a_s;
+            a_ai = a_a;
+            bi = bf;
+            const double x1 = -log(uniform(rng));
+            const double wc = fdiv(w, bias);
+            if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) { /* :985 */
+                const double frac = fdiv(x1, bias * d_tau_scatt);
+                d_tau_abs *= frac;
+                if (d_tau_abs > 100) { /* absorbed before scattering */
+                    ended = true;
+                    reason = 2;
+                    break;
+                }
+                d_tau_scatt *= frac;
+                const double d_tau = d_tau_abs + d_tau_scatt;
+                if (d_tau_abs < 1.0e-3)
+                    w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+                else
+                    w *= exp(-d_tau);
+                /* photon_2 pushed to the scattering point (:1005-1010) */
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    x[i] = x2[i];
+                    k[i] = k2[i];
+                    dk[i] = dk2[i];
+                }
+                e_0_s = e0s2;
+                walk_push(P, x, k, dk, e_0_s, dl * frac, 0, 0u, rank, 0);
+                zone_fetch(P, x, Z);
+                trig_at(P, x, T);
+                gcov_from_trig(P, T, G);
+                fluid_from(P, x, G, Z, F);
+                fl_ne = F.n_e;
+                if (F.n_e > 0.0 && (k[0] > 1.0e5 || k[0] < 0.0 || isnan(k[0]) || isnan(k[1]) || isnan(k[3]))) {
+                    /* scatter_super_photon's parent-side check (:1076-1081, :1018-1021) */
+                    k[0] = fabs(k[0]);
+                    w = 0.0;
+                    ended = true;
+                    reason = 2;
+                    break;
+                }
+                const double nu2 = fluid_nu(k, F);
+                double a_s2 = 0.0, a_a2 = 0.0;
+                if (!(nu2 < 0.0)) radiation_coeffs(P, k, F, nu2, a_s2, a_a2);
+                const double bf2 = bias_func(bias_d, F.theta_e, w);
+                if (F.n_e > 0.0) { /* the child (:1015-1024): to the overflow pool, tracked by the relaunch */
+                    if (own) push_overflow(C, x, k, rng, n_scatt, cold, F, wc);
+                    ++children;
+                }
+                a_si = a_s2;
+                a_ai = a_a2;
+                bi = bf2;
+            } else {
+                if (d_tau_abs > 100) { /* absorbed */
+                    ended = true;
+                    reason = 2;
+                    break;
+                }
+                const double d_tau = d_tau_abs + d_tau_scatt;
+                if (d_tau < 1.0e-3)
+                    w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
+                else
+                    w *= exp(-d_tau);
+            }
+            tau_abs += d_tau_abs;
+            tau_scatt += d_tau_scatt;
+        }
+        ++n_step; /* :1058-1063 */
+        if (n_step > MAX_N_STEP) {
+            ended = true;
+            reason = 3;
+            break;
+        }
+    }
+    if (own) {
+        if (abandoned) {
+            const unsigned long long slot = atomicAdd(C.stuck_count, 1ull);
+            if (slot < C.stuck_cap) {
+                double *r = C.stuck + slot * STUCK_WORDS;
+                r[0] = (double)rng.id;
+                r[1] = n_step;
+                r[2] = r[3] = r[4] = r[7] = 0.0;
+                r[5] = w;
+                r[6] = e_0_s;
+                for (int i = 0; i < 4; ++i) {
+                    r[8 + i] = x[i];
+                    r[12 + i] = k[i];
+                }
+            }
+            atomicAdd(&C.ctr->n_abandoned, 1ull);
+        } else if (ended) {
+            /* record_criterion (:1066) when the stop criterion ended it, else the reason's trace */
+            if (reason < 0 && x[1] > P.x1_max && n_step <= MAX_N_STEP)
+                record_photon(P, C, cold, rng.id, w, x[1], x[2], x[3], tau_abs, tau_scatt, n_scatt, n_step,
+                              reinterpret_cast<double *>(C.spec), (int)(sizeof(grm_spectrum_cell) / sizeof(double)));
+            else if (C.trace)
+                write_trace(C, cold, rng.id, w, x[1], x[2], x[3], tau_abs, tau_scatt, n_scatt, n_step,
+                            reason < 0 ? 2 : reason, -1, -1);
+        }
+        flush_counters(C);
+        atomicAdd(&C.ctr->n_steps, steps);
+        if (children) atomicAdd(&C.ctr->n_children, children);
+        atomicMax(&C.ctr->max_nstep, (unsigned long long)n_step);
+        if (n_step > 100000) atomicAdd(&C.ctr->n_long, 1ull);
     }
 }
 
@@ -767,7 +1069,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             /* the child leaves as a scatter request; its stores go out after this trip's table
              * loads, so no load of the trip waits behind them (vmcnt is in order) */
             if (F.n_e > 0.0) {
-                if (push_request(C, L, cold, F, L.p_wc(), wstack, wtop)) ++L.flight();
+                if (push_request(C, L.x, L.k, L.rng, L.n_scatt(), cold, F, L.p_wc(), wstack, wtop)) ++L.flight();
                 ++L.c_children();
             }
             L.alpha_scatti() = a_s;
@@ -885,6 +1187,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     L.rng.k1 = C.key1;
     bool active = false;
     bool pool_done = false;      /* wave-uniform */
+    unsigned long long res_next = 0, res_end = 0; /* wave-uniform: reserved claim positions */
+    bool head_done = false;      /* wave-uniform: the pool head has passed pos_end */
     bool warm = C.admit_n != 0;  /* wave-uniform: warm-up admission in force */
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
     L.flight() = 0;
@@ -1004,17 +1308,28 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                         }
                         if (__shfl(off, 0)) {
                             warm = false; /* admission over: plain claims from here on */
-                            if (lane_id == 0) base = atomicAdd(C.pool_head, (unsigned long long)k_pool);
-                            base = __shfl(base, 0);
                         } else {
                             base = __shfl(base, 0);
                             k_pool = (int)__shfl(got, 0);
+                            if (k_pool > 0 && base + k_pool >= C.pos_end) pool_done = true;
                         }
-                        if (k_pool > 0 && base + k_pool >= C.pos_end) pool_done = true;
-                    } else {
-                        if (lane_id == 0) base = atomicAdd(C.pool_head, (unsigned long long)k_pool);
-                        base = __shfl(base, 0);
-                        if (base + k_pool >= C.pos_end) pool_done = true;
+                    }
+                    if (!warm) {
+                        /* the wave's reservation of claim positions: one global atomic per RES_CHUNK
+                         * positions instead of one per refill (2048 waves refilling a few lanes every
+                         * ~20 trips would queue on the pool head's single address) */
+                        if (res_next >= res_end) {
+                            unsigned long long b = 0;
+                            if (lane_id == 0) b = atomicAdd(C.pool_head, (unsigned long long)RES_CHUNK);
+                            b = __shfl(b, 0);
+                            res_next = b;
+                            res_end = min(b + RES_CHUNK, C.pos_end);
+                            head_done = b + RES_CHUNK >= C.pos_end;
+                        }
+                        base = res_next;
+                        k_pool = res_end > res_next ? (int)min((unsigned long long)k_pool, res_end - res_next) : 0;
+                        res_next += k_pool;
+                        if (head_done && res_next >= res_end) pool_done = true;
                     }
                 }
                 if (lane_id == 0) *wtop = top - k_child;
@@ -1079,12 +1394,26 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             continue;
         }
         wait_trips = 0;
-        /* tail speculation (halving_walk): this wave's only work left is one photon in a push */
+        /* the tail: this wave's only work left is one photon -- run it with the whole wave (lone_run
+         * from the top of a step; halving_walk to finish a push already in progress) */
         bool walked = false, ended = false;
         if (pool_done && !warm) {
             const unsigned long long act = __ballot(active);
             if (__popcll(act) == 1 && *wtop == 0) {
                 const int owner = __ffsll((long long)act) - 1;
+                if (__builtin_amdgcn_readlane(L.phase, owner) == 0 && C.lone) {
+                    /* hand the photon over to the lone kernel (one wave per photon, after this launch) */
+                    unsigned long long slot = 0;
+                    if (active) slot = atomicAdd(C.lone_count, 1ull);
+                    slot = __shfl(slot, owner);
+                    if (slot < C.lone_cap) {
+                        if (active) {
+                            export_lone(C.lone + slot, L, cold);
+                            active = false;
+                        }
+                        continue;
+                    }
+                }
                 int walk = 0;
                 if (active) {
                     if (L.phase == 0 && !trip_begin(P, C, L, cold, ph2))
@@ -1096,6 +1425,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                     halving_walk(P, L, owner);
                     walked = true;
                 }
+            }
+        }
+        if (C.lone_all && active && L.phase == 0) {
+            const unsigned long long slot = atomicAdd(C.lone_count, 1ull);
+            if (slot < C.lone_cap) {
+                export_lone(C.lone + slot, L, cold);
+                active = false;
             }
         }
         if (active) {
@@ -1207,6 +1543,9 @@ struct grm_engine {
     int64_t watchdog_ms = 60000;           /* per-launch watchdog (GRM_OPT_WATCHDOG_MS; 0 = off) */
     double *d_stuck = nullptr;             /* [STUCK_CAP][STUCK_WORDS] abandoned-photon records */
     double *d_spec_blocks = nullptr;       /* per-workgroup spectrum slices */
+    LoneRec *d_lone = nullptr;             /* photons handed over to lone_kernel */
+    unsigned long long lone_cap = 0;
+    int lone = 1;                          /* GRM_OPT_LONE */
     /* pinned host staging for the per-pass small transfers: resets are H2D copies from pin->zero and
      * readbacks land in pin->ctr / pin->word, all on the engine stream -- DMA engine transfers, where
      * pageable copies and hipMemset would each need a blit/fill kernel, i.e. a free CU, which with
@@ -1280,6 +1619,12 @@ int alloc_lanes(grm_engine *e) {
         e->d_spec_blocks = nullptr;
         HIPCHK(e, hipMalloc(&e->d_spec_blocks, (size_t)grid * SPEC_LDS * sizeof(double)));
         HIPCHK(e, hipMemset(e->d_spec_blocks, 0, (size_t)grid * SPEC_LDS * sizeof(double)));
+        /* at most one hand-over per wave per launch (one per lane and launch's photon in the test
+         * mode GRM_OPT_LONE = 2, sized in run_passes) */
+        if (e->d_lone) (void)hipFree(e->d_lone);
+        e->d_lone = nullptr;
+        e->lone_cap = lanes / 64;
+        HIPCHK(e, hipMalloc(&e->d_lone, e->lone_cap * sizeof(LoneRec)));
         e->lanes = lanes;
     }
     e->grid = grid;
@@ -1304,6 +1649,12 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     if (pos1 <= pos0) return 0;
     /* overflow pool: children rarely spill (8-deep lane stacks); size ~ max(1M, n/4) */
     if (ensure_ovf(e, std::max<unsigned long long>(1ull << 20, (pos1 - pos0) / 4))) return -1;
+    if (e->lone == 2 && e->lone_cap < e->ovf_cap + n) { /* test mode: every photon may be handed over */
+        if (e->d_lone) (void)hipFree(e->d_lone);
+        e->d_lone = nullptr;
+        e->lone_cap = e->ovf_cap + n;
+        HIPCHK(e, hipMalloc(&e->d_lone, e->lone_cap * sizeof(LoneRec)));
+    }
     Ctl C{};
     C.pool = d_batch;
     C.pool_kind = 0;
@@ -1335,6 +1686,10 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.stuck = e->d_stuck;
     C.stuck_cap = STUCK_CAP;
     C.stuck_count = e->d_small + 6;
+    C.lone = e->lone ? e->d_lone : nullptr;
+    C.lone_cap = e->lone_cap;
+    C.lone_count = e->d_small + 7;
+    C.lone_all = e->lone == 2;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
@@ -1395,19 +1750,40 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.pool_sh = 0;
             C.admit_n = 0;
         }
-        if (zero_async(e, &e->d_ctr->abort, sizeof(unsigned long long))) return -1;
+        if (zero_async(e, &e->d_ctr->abort, sizeof(unsigned long long)) ||
+            zero_async(e, e->d_small + 7, sizeof(unsigned long long)))
+            return -1;
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
         hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+        HIPCHK(e, hipMemcpyAsync(&e->pin->word[5], e->d_small + 7, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        float ms = 0.f;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+        ms_total += ms;
+        const unsigned long long n_lone = std::min<unsigned long long>(e->pin->word[5], e->lone_cap);
+        if (n_lone) {
+            /* the photons the launch handed over, one wave each; their children join this launch's
+             * overflow pool */
+            HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+            hipLaunchKernelGGL(lone_kernel, dim3((unsigned)n_lone), dim3(64), 0, e->stream, e->P, C, n_lone);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            float ms_l = 0.f;
+            HIPCHK(e, hipEventElapsedTime(&ms_l, e->ev0, e->ev1));
+            ms_total += ms_l;
+            e->stats.lone_ms += ms_l;
+            e->stats.n_lone += n_lone;
+            e->stats.n_launches++;
+        }
         HIPCHK(e, hipMemcpyAsync(&e->pin->word[0], C.ovf_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                  e->stream));
         DevCounters hp;
         if (read_counters(e, hp)) return -1;
         const unsigned long long cnt = e->pin->word[0];
-        float ms = 0.f;
-        HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
-        ms_total += ms;
         if (ms > e->stats.max_launch_ms) { /* the dominant launch of this transport call */
             e->stats.max_launch_ms = ms;
             e->stats.max_launch_steps = hp.n_steps - steps_pass;
@@ -1597,6 +1973,7 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_small);
     hipFree(e->d_stuck);
     hipFree(e->d_spec_blocks);
+    hipFree(e->d_lone);
     if (e->pin) hipHostFree(e->pin);
     hipFree(e->d_batch);
     hipFree(e->d_trace);
@@ -1641,6 +2018,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_REFILL_MIN: e->refill_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_CHILD_MIN: e->child_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_WARMUP_SLACK: e->warmup_slack = v < 0 ? 0 : (v > 30 ? 30 : (int)v); return 0;
+    case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }

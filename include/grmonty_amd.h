@@ -117,6 +117,8 @@ typedef struct grm_stats {
     uint64_t n_long_photons;   /* superphotons that lived more than 100k steps since the last reset */
     uint64_t n_abandoned;      /* photons dropped by the launch watchdog (GRM_OPT_WATCHDOG_MS); 0 in a good run */
     uint64_t n_nan_photons;    /* superphotons ended at a NaN position since the last reset (see grm_engine.hip) */
+    uint64_t n_lone;           /* photons handed over to the lone-photon kernel since the last reset */
+    double lone_ms;            /* time in lone-photon kernel launches since the last reset */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
@@ -149,7 +151,11 @@ enum {
      * scattering sampling, more idle lane-trips while a batch gathers */
     GRM_OPT_CHILD_MIN = 11,
     /* warm-up straggler tolerance, log2 (default 4: 1/16 of the history may still be in flight) */
-    GRM_OPT_WARMUP_SLACK = 12
+    GRM_OPT_WARMUP_SLACK = 12,
+    /* 1 (default): a wave whose only work left is one photon hands it to the lone-photon kernel (one
+     * wave per photon, after the launch); 0: the lane loop keeps it; 2: every photon is handed over
+     * at the top of its first step (tests of the lone-photon path) */
+    GRM_OPT_LONE = 13
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

@@ -316,7 +316,9 @@ static double dnd_gamma_e_k(double theta_e, double gamma_e, double k2f) { /* hot
 }
 
 /* hotcross.cpp:108-142; the dnd_gamma_e factor depends only on (theta_e, gamma_e) and is hoisted (same bits) */
+static uint64_t g_dbg_hcnum = 0, g_dbg_hclkup = 0;
 double hotcross_num(double w, double theta_e) {
+    ++g_dbg_hcnum;
     if (std::isnan(w)) return 0.0;
     if (theta_e < HC_MIN_T && w < HC_MIN_W) return SIGMA_THOMSON;
     if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
@@ -741,6 +743,7 @@ static Fluid fluid_zone(const grmo_model *m, int i, int j) {
 /* radiation.cpp:59-146, hotcross.cpp:81-106, jnu_mixed.cpp:75-158            */
 /* ------------------------------------------------------------------------- */
 static double hotcross_lkup(const grmo_model *m, double w, double theta_e) {
+    ++g_dbg_hclkup;
     if (w * theta_e < 1.0e-6) return SIGMA_THOMSON;
     if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
     if (w <= HC_MIN_W || w >= HC_MAX_W || theta_e <= HC_MIN_T || theta_e >= HC_MAX_T) return hotcross_num(w, theta_e);
@@ -909,6 +912,10 @@ static void sample_rand_dir(Rng &r, double &x, double &y, double &z) { /* :202-2
     y = std::sqrt(1.0 - z * z) * sep_sin(phi);
 }
 
+/* rejection-loop statistics of the scattering samplers (diagnostics): [0] calls, [1] outer
+ * (Klein-Nishina) iterations, [2] y iterations, [3] max outer per call, [4..35] log2 histogram of
+ * y iterations per call */
+static uint64_t g_dbg_samp[40];
 static double sample_y_distr(Rng &r, double theta_e) { /* :123-166 */
     double pi_3 = std::sqrt(kPi) / 4.0;
     double pi_4 = std::sqrt(0.5 * theta_e) / 2.0;
@@ -937,6 +944,7 @@ static double sample_y_distr(Rng &r, double theta_e) { /* :123-166 */
         const double num = std::sqrt(1.0 + 0.5 * theta_e * y * y);
         const double den = (1.0 + y * std::sqrt(0.5 * theta_e));
         prob = num / den;
+        ++g_dbg_samp[2];
     } while (x2 >= prob);
     return y;
 }
@@ -949,7 +957,11 @@ static double sample_mu_distr(Rng &r, double beta_e) { /* :168-172 */
 
 static void sample_electron(Rng &r, const double k[4], double p[4], double theta_e) { /* :30-112 */
     double sigma_kn, gamma_e, beta_e, mu, x1;
+    const uint64_t y0 = g_dbg_samp[2];
+    uint64_t outer = 0;
+    ++g_dbg_samp[0];
     do {
+        ++outer;
         const double y = sample_y_distr(r, theta_e); /* sample_beta_distr :114-121 */
         gamma_e = y * y * theta_e + 1.0;
         beta_e = std::sqrt(1.0 - 1.0 / (gamma_e * gamma_e));
@@ -966,6 +978,17 @@ static void sample_electron(Rng &r, const double k[4], double p[4], double theta
                                                   (k_ * k_ - 2.0 * k_ - 2.0) / (2.0 * k_) * std::log(1.0 + 2.0 * k_));
         x1 = r.uniform();
     } while (x1 >= sigma_kn);
+    g_dbg_samp[1] += outer;
+    if (outer > g_dbg_samp[3]) g_dbg_samp[3] = outer;
+    {
+        uint64_t yi = g_dbg_samp[2] - y0;
+        int b = 0;
+        while (yi > 1 && b < 31) {
+            yi >>= 1;
+            ++b;
+        }
+        ++g_dbg_samp[4 + b];
+    }
     double v0x = k[1], v0y = k[2], v0z = k[3];
     const double v0 = std::sqrt(v0x * v0x + v0y * v0y + v0z * v0z);
     v0x /= v0;
@@ -2041,6 +2064,14 @@ size_t grmo_sizeof(int which) {
 }
 
 } /* extern "C" */
+/* hot cross-section lookups and their numerical-quadrature fallbacks (hotcross.cpp:81-142) so far */
+extern "C" void grmo_dbg_hotcross_stats(uint64_t out[2]) {
+    out[0] = g_dbg_hclkup;
+    out[1] = g_dbg_hcnum;
+}
+
+extern "C" void grmo_dbg_sampler_stats(uint64_t out[40]) { std::memcpy(out, g_dbg_samp, sizeof(g_dbg_samp)); }
+
 extern "C" void grmo_dbg_push_stats(uint64_t out[3]) {
     out[0] = g_dbg_attempts;
     out[1] = g_dbg_iter2;

@@ -123,6 +123,8 @@ def lib():
             "grmo_report_spectrum": (C.c_int, [vp, C.c_char_p, DP]),
             "grmo_sizeof": (C.c_size_t, [C.c_int]),
             "grmo_dbg_push_stats": (None, [U64P]),
+            "grmo_dbg_hotcross_stats": (None, [U64P]),
+            "grmo_dbg_sampler_stats": (None, [U64P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
