@@ -715,31 +715,26 @@ struct alignas(16) LoneRec {
 static_assert(sizeof(LoneRec) == 272, "LoneRec layout");
 
 __device__ __forceinline__ void export_lone(LoneRec *r, const Lane &L, const Cold *cold) {
-    LoneRec R;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        R.x[i] = L.x[i];
-        R.k[i] = L.k[i];
-        R.dk[i] = L.dk[i];
-    }
-    R.w = L.w;
-    R.e_0_s = L.e_0_s;
-    R.tau_abs = L.tau_abs();
-    R.tau_scatt = L.tau_scatt();
-    R.a_si = L.alpha_scatti();
-    R.a_ai = L.alpha_absi();
-    R.bi = L.bi();
-    R.fl_ne = L.fl_ne();
-    R.c = *cold;
-    R.id = L.rng.id;
-    R.ctr = L.rng.ctr;
-    R.n_step = L.n_step;
-    R.n_scatt = L.n_scatt();
-    R.pad = 0;
-    const double2 *s = reinterpret_cast<const double2 *>(&R);
+    /* field by field (a LoneRec built in registers first would add 68 VGPRs at this point of the loop) */
     double2 *d = reinterpret_cast<double2 *>(r);
+    d[0] = make_double2(L.x[0], L.x[1]);
+    d[1] = make_double2(L.x[2], L.x[3]);
+    d[2] = make_double2(L.k[0], L.k[1]);
+    d[3] = make_double2(L.k[2], L.k[3]);
+    d[4] = make_double2(L.dk[0], L.dk[1]);
+    d[5] = make_double2(L.dk[2], L.dk[3]);
+    d[6] = make_double2(L.w, L.e_0_s);
+    d[7] = make_double2(L.tau_abs(), L.tau_scatt());
+    d[8] = make_double2(L.alpha_scatti(), L.alpha_absi());
+    d[9] = make_double2(L.bi(), L.fl_ne());
+    const double2 *c = reinterpret_cast<const double2 *>(cold);
 #pragma unroll
-    for (int q = 0; q < (int)(sizeof(LoneRec) / 16); ++q) d[q] = s[q];
+    for (int q = 0; q < 5; ++q) d[10 + q] = c[q];
+    r->id = L.rng.id;
+    r->ctr = L.rng.ctr;
+    r->n_step = L.n_step;
+    r->n_scatt = L.n_scatt();
+    r->pad = 0;
 }
 
 /* the child of a lone photon's scattering, straight to the overflow pool */
@@ -750,15 +745,62 @@ __device__ __forceinline__ void push_overflow(const Ctl &C, const double x[4], c
     push_overflow_req(C, R);
 }
 
-/* one wave (64-thread block) per handed-over photon */
-__global__ __launch_bounds__(64) void lone_kernel(Params P, Ctl C, unsigned long long n) {
+/* Two waves per handed-over photon, pipelined: the geometry wave (wave 1) runs the photon's
+ * geodesic ahead -- photon_2, step size, push as a halving walk over its lanes (:920-930) -- into a
+ * ring of LONE_RING steps in LDS; the interaction wave (wave 0) consumes them in order and does
+ * everything else of the loop body: the stop criteria with their roulette draws, fluid, absorption
+ * and scattering coefficients, bias, the scattering decision, the weight (:919, :932-1063).  The
+ * geodesic does not depend on the interactions except at a scattering, where the photon continues
+ * from photon_2 pushed to the scattering point (:1005-1010): the interaction wave makes that push
+ * itself and restarts the geometry wave from it (a new generation; steps of the old one are
+ * discarded by their tag).  Both halves of a step then run at once on two SIMDs. */
+constexpr int LONE_RING = 32, LONE_BATCH = 16;
+struct LoneSlot {
+    double in[13], out[13]; /* photon_2 (x, k, dk/dlambda, e_0_s) and the state after the push */
+    double dl;
+    unsigned long long tag; /* (generation << 32) | (step index + 1), stored last */
+};
+struct LoneCtl {
+    unsigned long long cons, req, stop; /* steps consumed; restart request (generation << 32 | step); end */
+    double rs[13];                      /* restart state */
+};
+__shared__ LoneSlot s_ring[LONE_RING];
+__shared__ LoneCtl s_lctl;
+
+__device__ __forceinline__ void pack13(volatile double *d, const double x[4], const double k[4], const double dk[4],
+                                       double e) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        d[i] = x[i];
+        d[4 + i] = k[i];
+        d[8 + i] = dk[i];
+    }
+    d[12] = e;
+}
+
+__device__ __forceinline__ void unpack13(const volatile double *d, double x[4], double k[4], double dk[4], double &e) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[i] = d[i];
+        k[i] = d[4 + i];
+        dk[i] = d[8 + i];
+    }
+    e = d[12];
+}
+
+__global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned long long n) {
     if (blockIdx.x >= n) return;
-    const int lane = (int)threadIdx.x;
-    const bool own = lane == 0;
-    const int rank = lane;
-    if (lane < 4) s_cnt[0][lane] = 0;
-    __syncthreads();
+    const int wave = (int)(threadIdx.x >> 6);
+    const int lane = (int)(threadIdx.x & 63);
     const LoneRec &R = C.lone[blockIdx.x];
+    if (threadIdx.x < 4) s_cnt[0][threadIdx.x] = 0;
+    if (threadIdx.x < LONE_RING) s_ring[threadIdx.x].tag = 0;
+    if (threadIdx.x == 0) {
+        s_lctl.cons = 0;
+        s_lctl.req = 0;
+        s_lctl.stop = 0;
+    }
+    __syncthreads();
     double x[4], k[4], dk[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -766,7 +808,47 @@ __global__ __launch_bounds__(64) void lone_kernel(Params P, Ctl C, unsigned long
         k[i] = R.k[i];
         dk[i] = R.dk[i];
     }
-    double w = R.w, e_0_s = R.e_0_s;
+    double e_0_s = R.e_0_s;
+    if (wave == 1) {
+        /* ---- geometry wave ---- */
+        unsigned gen = 0;
+        unsigned long long p = 0;
+        while (true) {
+            if (__hip_atomic_load(&s_lctl.stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+            const unsigned long long req = __hip_atomic_load(&s_lctl.req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((unsigned)(req >> 32) != gen) { /* restart from the scattering point */
+                gen = (unsigned)(req >> 32);
+                p = req & 0xffffffffull;
+                unpack13(s_lctl.rs, x, k, dk, e_0_s);
+            }
+            if (p >= __hip_atomic_load(&s_lctl.cons, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + LONE_RING) {
+#ifdef GRM_TIMING
+                const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+                __builtin_amdgcn_s_sleep(1); /* the ring is full */
+                if (lane == 0) atomicAdd(C.timing + 15, __builtin_amdgcn_s_memtime() - t0);
+#else
+                __builtin_amdgcn_s_sleep(1); /* the ring is full */
+#endif
+                continue;
+            }
+            LoneSlot &S = s_ring[p % LONE_RING];
+            if (lane == 0) pack13(S.in, x, k, dk, e_0_s);
+            const double dl = step_size(P, x, k);
+            walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, lane, 0);
+            if (lane == 0) {
+                pack13(S.out, x, k, dk, e_0_s);
+                S.dl = dl;
+                __hip_atomic_store(&S.tag, ((unsigned long long)gen << 32) | (p + 1), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            ++p;
+        }
+        return;
+    }
+    /* ---- interaction wave ---- */
+    const bool own = lane == 0;
+    const int rank = lane;
+    double w = R.w;
     double tau_abs = R.tau_abs, tau_scatt = R.tau_scatt, a_si = R.a_si, a_ai = R.a_ai, bi = R.bi, fl_ne = R.fl_ne;
     const Cold *cold = &R.c;
     int n_step = R.n_step;
@@ -782,148 +864,195 @@ __global__ __launch_bounds__(64) void lone_kernel(Params P, Ctl C, unsigned long
     unsigned long long steps = 0, children = 0;
     bool ended = false, abandoned = false;
     int reason = -1; /* ended without a record: trace reason */
-    for (unsigned s = 1;; ++s) {
-        if ((s & (REFRESH_TRIPS - 1)) == 0) {
-            flush_counters(C);
-            if (!C.bias_frozen) bias_d = bias_den(P, C);
-            if (C.watchdog_ticks) {
-                bool stop = __hip_atomic_load(&C.ctr->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                if (!stop && __builtin_amdgcn_s_memrealtime() - rt_start > C.watchdog_ticks) {
-                    stop = true;
-                    if (own) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if (stop) {
-                    abandoned = true;
-                    break;
-                }
-            }
+    unsigned gen = 0;
+    unsigned long long si = 0; /* index of the next step */
+    unsigned s = 0;            /* steps since the kernel start (refresh period) */
+    bool done = false;
+    while (!done) {
+        /* A batch: the consecutive steps the geometry wave has ready (at least one, at most
+         * LONE_BATCH).  Lane j evaluates the fluid and the absorption / scattering coefficients at
+         * the end point of step si + j at once -- the same code for every lane, and these depend on
+         * the geodesic only -- then the steps' interactions run in order, each taking its lane's
+         * values; a scattering discards the rest of the batch (the photon continues elsewhere). */
+        const unsigned long long base = si;
+        {
+            LoneSlot &S0 = s_ring[base % LONE_RING];
+            const unsigned long long want = ((unsigned long long)gen << 32) | (base + 1);
+#ifdef GRM_TIMING
+            const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+#endif
+            while (__hip_atomic_load(&S0.tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != want)
+                __builtin_amdgcn_s_sleep(1);
+#ifdef GRM_TIMING
+            if (own) atomicAdd(C.timing + 14, __builtin_amdgcn_s_memtime() - tw0);
+#endif
         }
-        /* while (!stop_criterion(photon)) (:919) */
-        if (stop_criterion(P, x[1], w, rng)) {
-            ended = true;
-            break;
-        }
-        /* photon_2 (:920-925), step size, push (:927-930) */
-        double x2[4], k2[4], dk2[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            x2[i] = x[i];
-            k2[i] = k[i];
-            dk2[i] = dk[i];
-        }
-        const double e0s2 = e_0_s;
-        const double dl = step_size(P, x, k);
-        walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, rank, 0);
-        ++steps;
-        if (stop_criterion(P, x[1], w, rng)) { /* :932-934 */
-            ended = true;
-            break;
-        }
-        if (isnan(x[1])) { /* a NaN position is absorbing (see transport_trip) */
-            if (own) atomicAdd(&C.ctr->n_nan, 1ull);
-            ended = true;
-            reason = 3;
-            break;
-        }
-        if (a_ai > 0.0 || a_si > 0.0 || fl_ne > 0.0) { /* :937 */
+        const unsigned long long qj = base + (lane < LONE_BATCH ? lane : 0);
+        const bool ready = lane < LONE_BATCH && __hip_atomic_load(&s_ring[qj % LONE_RING].tag, __ATOMIC_ACQUIRE,
+                                                                  __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                                                    (((unsigned long long)gen << 32) | (qj + 1));
+        const unsigned long long rb = __ballot(ready);
+        const int nb = rb == ~0ull ? 64 : __ffsll((long long)~rb) - 1; /* leading run of ready steps (>= 1) */
+        double l_ne, l_te, l_as = 0.0, l_aa = 0.0;
+        int l_zero;
+        {
+            const LoneSlot &Sj = s_ring[(base + (lane < nb ? lane : 0)) % LONE_RING];
+            double xj[4], kj[4], dkj[4], ej;
+            unpack13(Sj.out, xj, kj, dkj, ej);
             Trig T;
             Gcov G;
             ZoneFetch Z;
-            zone_fetch(P, x, Z); /* issued first: its latency overlaps the metric */
-            trig_at(P, x, T);
+            zone_fetch(P, xj, Z);
+            trig_at(P, xj, T);
             gcov_from_trig(P, T, G);
             Fluid F;
-            fluid_from(P, x, G, Z, F);
-            fl_ne = F.n_e;
-            const double nu = fluid_nu(k, F);
-            const bool zero = nu < 0.0 || F.n_e == 0.0; /* bound_flag (:941-955) or nu < 0 */
-            double a_s = 0.0, a_a = 0.0;
-            if (!zero) radiation_coeffs(P, k, F, nu, a_s, a_a);
-            const double bf = zero ? 0.0 : bias_func(bias_d, F.theta_e, w);
-            double d_tau_scatt, d_tau_abs, bias;
-            if (zero) {
-                d_tau_scatt = 0.5 * a_si * P.d_tau_k * dl;
-                d_tau_abs = 0.5 * a_ai * P.d_tau_k * dl;
-                bias = 0.0;
-            } else {
-                d_tau_scatt = 0.5 * (a_si + a_s) * P.d_tau_k * dl;
-                d_tau_abs = 0.5 * (a_ai + a_a) * P.d_tau_k * dl;
-                bias = 0.5 * (bi + bf);
-            }
-            a_si = a_s;
-            a_ai = a_a;
-            bi = bf;
-            const double x1 = -log(uniform(rng));
-            const double wc = fdiv(w, bias);
-            if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) { /* :985 */
-                const double frac = fdiv(x1, bias * d_tau_scatt);
-                d_tau_abs *= frac;
-                if (d_tau_abs > 100) { /* absorbed before scattering */
-                    ended = true;
-                    reason = 2;
-                    break;
-                }
-                d_tau_scatt *= frac;
-                const double d_tau = d_tau_abs + d_tau_scatt;
-                if (d_tau_abs < 1.0e-3)
-                    w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
-                else
-                    w *= exp(-d_tau);
-                /* photon_2 pushed to the scattering point (:1005-1010) */
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    x[i] = x2[i];
-                    k[i] = k2[i];
-                    dk[i] = dk2[i];
-                }
-                e_0_s = e0s2;
-                walk_push(P, x, k, dk, e_0_s, dl * frac, 0, 0u, rank, 0);
-                zone_fetch(P, x, Z);
-                trig_at(P, x, T);
-                gcov_from_trig(P, T, G);
-                fluid_from(P, x, G, Z, F);
-                fl_ne = F.n_e;
-                if (F.n_e > 0.0 && (k[0] > 1.0e5 || k[0] < 0.0 || isnan(k[0]) || isnan(k[1]) || isnan(k[3]))) {
-                    /* scatter_super_photon's parent-side check (:1076-1081, :1018-1021) */
-                    k[0] = fabs(k[0]);
-                    w = 0.0;
-                    ended = true;
-                    reason = 2;
-                    break;
-                }
-                const double nu2 = fluid_nu(k, F);
-                double a_s2 = 0.0, a_a2 = 0.0;
-                if (!(nu2 < 0.0)) radiation_coeffs(P, k, F, nu2, a_s2, a_a2);
-                const double bf2 = bias_func(bias_d, F.theta_e, w);
-                if (F.n_e > 0.0) { /* the child (:1015-1024): to the overflow pool, tracked by the relaunch */
-                    if (own) push_overflow(C, x, k, rng, n_scatt, cold, F, wc);
-                    ++children;
-                }
-                a_si = a_s2;
-                a_ai = a_a2;
-                bi = bf2;
-            } else {
-                if (d_tau_abs > 100) { /* absorbed */
-                    ended = true;
-                    reason = 2;
-                    break;
-                }
-                const double d_tau = d_tau_abs + d_tau_scatt;
-                if (d_tau < 1.0e-3)
-                    w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
-                else
-                    w *= exp(-d_tau);
-            }
-            tau_abs += d_tau_abs;
-            tau_scatt += d_tau_scatt;
+            fluid_from(P, xj, G, Z, F);
+            const double nu = fluid_nu(kj, F);
+            l_zero = (nu < 0.0 || F.n_e == 0.0) ? 1 : 0; /* bound_flag (:941-955) or nu < 0 */
+            if (!l_zero) radiation_coeffs(P, kj, F, nu, l_as, l_aa);
+            l_ne = F.n_e;
+            l_te = F.theta_e;
         }
-        ++n_step; /* :1058-1063 */
-        if (n_step > MAX_N_STEP) {
-            ended = true;
-            reason = 3;
-            break;
+        for (int bj = 0; bj < nb; ++bj) {
+            if ((++s & (REFRESH_TRIPS - 1)) == 0) {
+                flush_counters(C);
+                if (!C.bias_frozen) bias_d = bias_den(P, C);
+                if (C.watchdog_ticks) {
+                    bool stop = __hip_atomic_load(&C.ctr->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    if (!stop && __builtin_amdgcn_s_memrealtime() - rt_start > C.watchdog_ticks) {
+                        stop = true;
+                        if (own) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (stop) {
+                        abandoned = done = true;
+                        break;
+                    }
+                }
+            }
+            /* while (!stop_criterion(photon)) (:919) */
+            if (stop_criterion(P, x[1], w, rng)) {
+                ended = done = true;
+                break;
+            }
+            /* photon_2, step size and push of this step: from the geometry wave */
+            const LoneSlot &S = s_ring[(base + bj) % LONE_RING];
+            double dkn[4], e_n;
+            unpack13(S.out, x, k, dkn, e_n);
+            const double dl = S.dl;
+            ++steps;
+            if (stop_criterion(P, x[1], w, rng)) { /* :932-934 */
+                ended = done = true;
+                break;
+            }
+            if (isnan(x[1])) { /* a NaN position is absorbing (see transport_trip) */
+                if (own) atomicAdd(&C.ctr->n_nan, 1ull);
+                ended = done = true;
+                reason = 3;
+                break;
+            }
+            bool restart = false;
+            if (a_ai > 0.0 || a_si > 0.0 || fl_ne > 0.0) { /* :937 */
+                const double n_e = bcast(l_ne, bj), t_e = bcast(l_te, bj);
+                const double a_s = bcast(l_as, bj), a_a = bcast(l_aa, bj);
+                const bool zero = __builtin_amdgcn_readlane(l_zero, bj) != 0;
+                fl_ne = n_e;
+                const double bf = zero ? 0.0 : bias_func(bias_d, t_e, w);
+                double d_tau_scatt, d_tau_abs, bias;
+                if (zero) {
+                    d_tau_scatt = 0.5 * a_si * P.d_tau_k * dl;
+                    d_tau_abs = 0.5 * a_ai * P.d_tau_k * dl;
+                    bias = 0.0;
+                } else {
+                    d_tau_scatt = 0.5 * (a_si + a_s) * P.d_tau_k * dl;
+                    d_tau_abs = 0.5 * (a_ai + a_a) * P.d_tau_k * dl;
+                    bias = 0.5 * (bi + bf);
+                }
+                a_si = a_s;
+                a_ai = a_a;
+                bi = bf;
+                const double x1 = -log(uniform(rng));
+                const double wc = fdiv(w, bias);
+                if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) { /* :985 */
+                    const double frac = fdiv(x1, bias * d_tau_scatt);
+                    d_tau_abs *= frac;
+                    if (d_tau_abs > 100) { /* absorbed before scattering */
+                        ended = done = true;
+                        reason = 2;
+                        break;
+                    }
+                    d_tau_scatt *= frac;
+                    const double d_tau = d_tau_abs + d_tau_scatt;
+                    if (d_tau_abs < 1.0e-3)
+                        w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+                    else
+                        w *= exp(-d_tau);
+                    /* photon_2 pushed to the scattering point (:1005-1010), by this wave */
+                    double dk[4], e_0_s;
+                    unpack13(S.in, x, k, dk, e_0_s);
+                    walk_push(P, x, k, dk, e_0_s, dl * frac, 0, 0u, rank, 0);
+                    Trig T;
+                    Gcov G;
+                    ZoneFetch Z;
+                    zone_fetch(P, x, Z);
+                    trig_at(P, x, T);
+                    gcov_from_trig(P, T, G);
+                    Fluid F;
+                    fluid_from(P, x, G, Z, F);
+                    fl_ne = F.n_e;
+                    if (F.n_e > 0.0 && (k[0] > 1.0e5 || k[0] < 0.0 || isnan(k[0]) || isnan(k[1]) || isnan(k[3]))) {
+                        /* scatter_super_photon's parent-side check (:1076-1081, :1018-1021) */
+                        k[0] = fabs(k[0]);
+                        w = 0.0;
+                        ended = done = true;
+                        reason = 2;
+                        break;
+                    }
+                    const double nu2 = fluid_nu(k, F);
+                    double a_s2 = 0.0, a_a2 = 0.0;
+                    if (!(nu2 < 0.0)) radiation_coeffs(P, k, F, nu2, a_s2, a_a2);
+                    const double bf2 = bias_func(bias_d, F.theta_e, w);
+                    if (F.n_e > 0.0) { /* the child (:1015-1024): to the overflow pool, tracked by the relaunch */
+                        if (own) push_overflow(C, x, k, rng, n_scatt, cold, F, wc);
+                        ++children;
+                    }
+                    a_si = a_s2;
+                    a_ai = a_a2;
+                    bi = bf2;
+                    /* the photon goes on from the scattering point: restart the geometry wave there */
+                    ++gen;
+                    if (own) {
+                        pack13(s_lctl.rs, x, k, dk, e_0_s);
+                        __hip_atomic_store(&s_lctl.req, ((unsigned long long)gen << 32) | (base + bj + 1),
+                                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    restart = true;
+                } else {
+                    if (d_tau_abs > 100) { /* absorbed */
+                        ended = done = true;
+                        reason = 2;
+                        break;
+                    }
+                    const double d_tau = d_tau_abs + d_tau_scatt;
+                    if (d_tau < 1.0e-3)
+                        w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
+                    else
+                        w *= exp(-d_tau);
+                }
+                tau_abs += d_tau_abs;
+                tau_scatt += d_tau_scatt;
+            }
+            ++n_step; /* :1058-1063 */
+            if (n_step > MAX_N_STEP) {
+                ended = done = true;
+                reason = 3;
+                break;
+            }
+            si = base + bj + 1;
+            if (own) __hip_atomic_store(&s_lctl.cons, si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (restart) break; /* the rest of the batch is on the old geodesic */
         }
     }
+    if (own) __hip_atomic_store(&s_lctl.stop, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (own) {
         if (abandoned) {
             const unsigned long long slot = atomicAdd(C.stuck_count, 1ull);
@@ -1394,26 +1523,28 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             continue;
         }
         wait_trips = 0;
-        /* the tail: this wave's only work left is one photon -- run it with the whole wave (lone_run
-         * from the top of a step; halving_walk to finish a push already in progress) */
+        /* the tail: this wave's only work left is one photon -- hand it to the lone-photon kernel at
+         * the top of a step (in the test mode GRM_OPT_LONE = 2: every photon at the top of its
+         * first step); halving_walk finishes a push already in progress with the whole wave */
         bool walked = false, ended = false;
-        if (pool_done && !warm) {
+        const bool tail = pool_done && !warm;
+        if (tail || C.lone_all) {
             const unsigned long long act = __ballot(active);
-            if (__popcll(act) == 1 && *wtop == 0) {
-                const int owner = __ffsll((long long)act) - 1;
-                if (__builtin_amdgcn_readlane(L.phase, owner) == 0 && C.lone) {
-                    /* hand the photon over to the lone kernel (one wave per photon, after this launch) */
-                    unsigned long long slot = 0;
-                    if (active) slot = atomicAdd(C.lone_count, 1ull);
-                    slot = __shfl(slot, owner);
-                    if (slot < C.lone_cap) {
-                        if (active) {
-                            export_lone(C.lone + slot, L, cold);
-                            active = false;
-                        }
-                        continue;
+            const bool alone = __popcll(act) == 1 && *wtop == 0;
+            if (C.lone && (alone || C.lone_all)) {
+                const bool hand = active && L.phase == 0;
+                if (__ballot(hand)) {
+                    unsigned long long slot = ~0ull;
+                    if (hand) slot = atomicAdd(C.lone_count, 1ull);
+                    if (hand && slot < C.lone_cap) {
+                        export_lone(C.lone + slot, L, cold);
+                        active = false;
                     }
+                    continue;
                 }
+            }
+            if (tail && alone) {
+                const int owner = __ffsll((long long)act) - 1;
                 int walk = 0;
                 if (active) {
                     if (L.phase == 0 && !trip_begin(P, C, L, cold, ph2))
@@ -1425,13 +1556,6 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                     halving_walk(P, L, owner);
                     walked = true;
                 }
-            }
-        }
-        if (C.lone_all && active && L.phase == 0) {
-            const unsigned long long slot = atomicAdd(C.lone_count, 1ull);
-            if (slot < C.lone_cap) {
-                export_lone(C.lone + slot, L, cold);
-                active = false;
             }
         }
         if (active) {
@@ -1768,7 +1892,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             /* the photons the launch handed over, one wave each; their children join this launch's
              * overflow pool */
             HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-            hipLaunchKernelGGL(lone_kernel, dim3((unsigned)n_lone), dim3(64), 0, e->stream, e->P, C, n_lone);
+            hipLaunchKernelGGL(lone_kernel, dim3((unsigned)n_lone), dim3(128), 0, e->stream, e->P, C, n_lone);
             HIPCHK(e, hipGetLastError());
             HIPCHK(e, hipEventRecord(e->ev1, e->stream));
             HIPCHK(e, hipStreamSynchronize(e->stream));

@@ -81,4 +81,6 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
                  11: "fluid", 12: "radiation", 13: "interact"}
         print("  timing: " + " ".join(f"{v}={tm[k] / tot:.3f}" for k, v in names.items()) +
               f" | trips/wave {tm[4]} child-refills {tm[5] / max(tm[4], 1):.4f} pool-refills "
-              f"{tm[6] / max(tm[4], 1):.4f} cycles/trip {tot / max(tm[4], 1):.0f}", flush=True)
+              f"{tm[6] / max(tm[4], 1):.4f} cycles/trip {tot / max(tm[4], 1):.0f} | lone kernel: {st['n_lone']} photons "
+          f"{st['lone_ms']:.1f} ms, interaction-wave wait {tm[14] / 2.4e6:.1f} ms geometry-wave wait "
+          f"{tm[15] / 2.4e6:.1f} ms (s_memtime at 2.4 GHz)", flush=True)
