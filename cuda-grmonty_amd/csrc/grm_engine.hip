@@ -635,8 +635,9 @@ __device__ __forceinline__ double bcast(double v, int src) {
 /* The halving walk proper, on a push state every lane of the wave holds identically (x, k, dk/dlambda,
  * e_0_s; the node `depth` of the halving tree being pushed, the pending second halves `pend`); lane
  * rank r (0 for the state's owner) attempts depth + r.  Leaves the completed push in every lane. */
-__device__ __forceinline__ void walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
-                                          double hlen, int depth, uint32_t pend, int rank, int owner) {
+__device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
+                                         double hlen, int depth, uint32_t pend, int rank, int owner) {
+    int rounds = 0; /* attempt rounds (diagnostics) */
     while (true) {
         if (!(x[1] < P.xs1)) {
             /* every lane attempts in place from the same start state; the winner's result is then
@@ -653,6 +654,7 @@ __device__ __forceinline__ void walk_push(const Params &P, double x[4], double k
             /* the owner's attempt if it passed, else the shallowest passing helper (helper depth grows
              * with lane index); some lane passes, since 63 helpers cover every depth to MAX_SUBDIV */
             const unsigned long long acc = __ballot(ok);
+            ++rounds;
             const int w = ((acc >> owner) & 1ull) ? owner : __ffsll((long long)acc) - 1;
             const int dw = __builtin_amdgcn_readlane(d, w);
 #pragma unroll
@@ -669,6 +671,7 @@ __device__ __forceinline__ void walk_push(const Params &P, double x[4], double k
         depth = 31 - __builtin_clz(pend);
         pend &= ~(1u << depth);
     }
+    return rounds;
 }
 
 __device__ __forceinline__ int walk_rank(int owner) {
@@ -755,19 +758,19 @@ __device__ __forceinline__ void push_overflow(const Ctl &C, const double x[4], c
  * itself and restarts the geometry wave from it (a new generation; steps of the old one are
  * discarded by their tag).  Both halves of a step then run at once on two SIMDs. */
 constexpr int LONE_RING = 32, LONE_BATCH = 16;
-struct LoneSlot {
-    double in[13], out[13]; /* photon_2 (x, k, dk/dlambda, e_0_s) and the state after the push */
-    double dl;
+constexpr unsigned long long LONE_STOP = ~0ull;
+struct alignas(16) LoneSlot {
+    double out[13], dl;     /* the state after the push (x, k, dk/dlambda, e_0_s) and the step size */
     unsigned long long tag; /* (generation << 32) | (step index + 1), stored last */
 };
-struct LoneCtl {
-    unsigned long long cons, req, stop; /* steps consumed; restart request (generation << 32 | step); end */
-    double rs[13];                      /* restart state */
+struct alignas(16) LoneCtl {
+    double rs[13];                /* restart state: photon_2 of the generation's first step */
+    unsigned long long cons, req; /* steps consumed; restart request (generation << 32 | step) or LONE_STOP */
 };
 __shared__ LoneSlot s_ring[LONE_RING];
 __shared__ LoneCtl s_lctl;
 
-__device__ __forceinline__ void pack13(volatile double *d, const double x[4], const double k[4], const double dk[4],
+__device__ __forceinline__ void pack13(double *d, const double x[4], const double k[4], const double dk[4],
                                        double e) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -778,7 +781,7 @@ __device__ __forceinline__ void pack13(volatile double *d, const double x[4], co
     d[12] = e;
 }
 
-__device__ __forceinline__ void unpack13(const volatile double *d, double x[4], double k[4], double dk[4], double &e) {
+__device__ __forceinline__ void unpack13(const double *d, double x[4], double k[4], double dk[4], double &e) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         x[i] = d[i];
@@ -793,14 +796,6 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned lon
     const int wave = (int)(threadIdx.x >> 6);
     const int lane = (int)(threadIdx.x & 63);
     const LoneRec &R = C.lone[blockIdx.x];
-    if (threadIdx.x < 4) s_cnt[0][threadIdx.x] = 0;
-    if (threadIdx.x < LONE_RING) s_ring[threadIdx.x].tag = 0;
-    if (threadIdx.x == 0) {
-        s_lctl.cons = 0;
-        s_lctl.req = 0;
-        s_lctl.stop = 0;
-    }
-    __syncthreads();
     double x[4], k[4], dk[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -809,36 +804,122 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned lon
         dk[i] = R.dk[i];
     }
     double e_0_s = R.e_0_s;
+    if (threadIdx.x < 4) s_cnt[0][threadIdx.x] = 0;
+    if (threadIdx.x < LONE_RING) s_ring[threadIdx.x].tag = 0;
+    if (threadIdx.x == 0) {
+        s_lctl.cons = 0;
+        s_lctl.req = 0;
+        pack13(s_lctl.rs, x, k, dk, e_0_s); /* the state before step 0 */
+    }
+    __syncthreads();
     if (wave == 1) {
         /* ---- geometry wave ---- */
         unsigned gen = 0;
-        unsigned long long p = 0;
+        unsigned long long p = 0, cur = 0, cons = 0; /* cons: the last value read of s_lctl.cons */
+        bool spec = false; /* speculate the halving depths on this step's push (the last one halved) */
+#ifdef GRM_TIMING
+        unsigned long long g_last = __builtin_amdgcn_s_memtime();
+        unsigned long long tg[6] = {0, 0, 0, 0, 0, 0}; /* steps, rounds, walk, step size, rest, halved */
+#endif
         while (true) {
-            if (__hip_atomic_load(&s_lctl.stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-            const unsigned long long req = __hip_atomic_load(&s_lctl.req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if ((unsigned)(req >> 32) != gen) { /* restart from the scattering point */
+            if (p + 1 >= cons + LONE_RING) { /* the slot of step p and that of p - 1 must be consumed */
+                cons = __hip_atomic_load(&s_lctl.cons, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (p + 1 >= cons + LONE_RING) {
+#ifdef GRM_TIMING
+                    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+                    __builtin_amdgcn_s_sleep(1); /* the ring is full */
+                    if (lane == 0) atomicAdd(C.timing + 15, __builtin_amdgcn_s_memtime() - t0);
+#else
+                    __builtin_amdgcn_s_sleep(1); /* the ring is full */
+#endif
+                    if (__hip_atomic_load(&s_lctl.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == cur) continue;
+                }
+            }
+            /* the restart request (stop folded in as LONE_STOP): read once per step and looked at
+             * after the push, so that its LDS latency hides behind it; a step computed while a
+             * restart was pending is dropped (and one published just before a restart carries the
+             * old generation's tag, which the interaction wave skips) */
+            const unsigned long long req = __hip_atomic_load(&s_lctl.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef GRM_TIMING
+            const unsigned long long g0 = __builtin_amdgcn_s_memtime();
+#endif
+            const double dl = step_size(P, x, k);
+#ifdef GRM_TIMING
+            const unsigned long long g1 = __builtin_amdgcn_s_memtime();
+#endif
+            /* Most steps pass their first attempt: then every lane makes that same attempt, the
+             * state stays identical over the wave and needs no broadcast.  A step that halves
+             * continues as a halving walk, and the next step speculates from the start. */
+            int rounds = 1;
+            {
+                if (!spec) {
+                    bool fail = false;
+                    if (!(x[1] < P.xs1)) {
+                        double xb[4], kb[4], dkb[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            xb[i] = x[i];
+                            kb[i] = k[i];
+                            dkb[i] = dk[i];
+                        }
+                        double e_1;
+                        Trig T;
+                        Gcov G;
+                        fail = push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
+                        if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                x[i] = xb[i];
+                                k[i] = kb[i];
+                                dk[i] = dkb[i];
+                            }
+                            rounds += walk_push(P, x, k, dk, e_0_s, dl, 1, 2u, lane, 0);
+                        } else {
+                            e_0_s = e_1;
+                        }
+                    }
+                    spec = fail;
+                } else {
+                    rounds = walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, lane, 0);
+                    spec = rounds > 1;
+                }
+            }
+            if (req != cur) {
+                if (req == LONE_STOP) {
+#ifdef GRM_TIMING
+                    /* slots 16-21: photons of > 1e5 steps (the tail), 22-27: the others */
+                    if (lane == 0)
+                        for (int r = 0; r < 6; ++r) atomicAdd(C.timing + (tg[0] > 100000 ? 16 : 22) + r, tg[r]);
+#endif
+                    break;
+                }
+                /* restart from the scattering point (this step, if computed, is on the old geodesic) */
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); /* rs was written before req */
+                cur = req;
                 gen = (unsigned)(req >> 32);
                 p = req & 0xffffffffull;
                 unpack13(s_lctl.rs, x, k, dk, e_0_s);
-            }
-            if (p >= __hip_atomic_load(&s_lctl.cons, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + LONE_RING) {
-#ifdef GRM_TIMING
-                const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-                __builtin_amdgcn_s_sleep(1); /* the ring is full */
-                if (lane == 0) atomicAdd(C.timing + 15, __builtin_amdgcn_s_memtime() - t0);
-#else
-                __builtin_amdgcn_s_sleep(1); /* the ring is full */
-#endif
+                spec = false;
                 continue;
             }
-            LoneSlot &S = s_ring[p % LONE_RING];
-            if (lane == 0) pack13(S.in, x, k, dk, e_0_s);
-            const double dl = step_size(P, x, k);
-            walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, lane, 0);
+#ifdef GRM_TIMING
+            const unsigned long long g2 = __builtin_amdgcn_s_memtime();
+            tg[0] += 1;
+            tg[1] += (unsigned long long)rounds;
+            tg[2] += g2 - g1;
+            tg[3] += g1 - g0;
+            tg[4] += g0 - g_last;
+            tg[5] += spec ? 1ull : 0ull;
+            g_last = g2;
+#endif
             if (lane == 0) {
+                LoneSlot &S = s_ring[p % LONE_RING];
                 pack13(S.out, x, k, dk, e_0_s);
                 S.dl = dl;
-                __hip_atomic_store(&S.tag, ((unsigned long long)gen << 32) | (p + 1), __ATOMIC_RELEASE,
+                /* LDS operations of a wave complete in order: the slot is written before its tag
+                 * (a compiler barrier keeps the stores in program order; no wait for completion) */
+                __asm__ volatile("" ::: "memory");
+                __hip_atomic_store(&S.tag, ((unsigned long long)gen << 32) | (p + 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             ++p;
@@ -865,7 +946,8 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned lon
     bool ended = false, abandoned = false;
     int reason = -1; /* ended without a record: trace reason */
     unsigned gen = 0;
-    unsigned long long si = 0; /* index of the next step */
+    unsigned long long gen_start = 0; /* the generation's first step */
+    unsigned long long si = 0;        /* index of the next step */
     unsigned s = 0;            /* steps since the kernel start (refresh period) */
     bool done = false;
     while (!done) {
@@ -988,7 +1070,9 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned lon
                         w *= exp(-d_tau);
                     /* photon_2 pushed to the scattering point (:1005-1010), by this wave */
                     double dk[4], e_0_s;
-                    unpack13(S.in, x, k, dk, e_0_s);
+                    /* photon_2 of this step: the state after the step before, or the restart state */
+                    unpack13(base + bj == gen_start ? s_lctl.rs : s_ring[(base + bj - 1) % LONE_RING].out, x, k, dk,
+                             e_0_s);
                     walk_push(P, x, k, dk, e_0_s, dl * frac, 0, 0u, rank, 0);
                     Trig T;
                     Gcov G;
@@ -1020,6 +1104,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned lon
                     bi = bf2;
                     /* the photon goes on from the scattering point: restart the geometry wave there */
                     ++gen;
+                    gen_start = base + bj + 1;
                     if (own) {
                         pack13(s_lctl.rs, x, k, dk, e_0_s);
                         __hip_atomic_store(&s_lctl.req, ((unsigned long long)gen << 32) | (base + bj + 1),
@@ -1052,7 +1137,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned lon
             if (restart) break; /* the rest of the batch is on the old geodesic */
         }
     }
-    if (own) __hip_atomic_store(&s_lctl.stop, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (own) __hip_atomic_store(&s_lctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (own) {
         if (abandoned) {
             const unsigned long long slot = atomicAdd(C.stuck_count, 1ull);
@@ -2073,8 +2158,8 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     P.zones = e->d_zones;
     P.hotcross = e->d_hot;
     P.k2 = e->d_k2;
-    if (!hip_ok(e, hipMalloc(&e->d_timing, 16 * sizeof(unsigned long long)), "timing") ||
-        !hip_ok(e, hipMemset(e->d_timing, 0, 16 * sizeof(unsigned long long)), "timing"))
+    if (!hip_ok(e, hipMalloc(&e->d_timing, 32 * sizeof(unsigned long long)), "timing") ||
+        !hip_ok(e, hipMemset(e->d_timing, 0, 32 * sizeof(unsigned long long)), "timing"))
         return fail();
     if (reset_counters(e)) return fail();
     *out = e;
@@ -2311,11 +2396,11 @@ int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm
     return 0;
 }
 
-int grm_engine_debug_timing(grm_engine *e, uint64_t out[16], int reset) {
+int grm_engine_debug_timing(grm_engine *e, uint64_t out[32], int reset) {
     if (!e || !out) return -1;
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, hipMemcpy(out, e->d_timing, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    if (reset) HIPCHK(e, hipMemset(e->d_timing, 0, 16 * sizeof(unsigned long long)));
+    HIPCHK(e, hipMemcpy(out, e->d_timing, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(e, hipMemset(e->d_timing, 0, 32 * sizeof(unsigned long long)));
 #ifdef GRM_TIMING
     return 1;
 #else

@@ -84,3 +84,10 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
               f"{tm[6] / max(tm[4], 1):.4f} cycles/trip {tot / max(tm[4], 1):.0f} | lone kernel: {st['n_lone']} photons "
           f"{st['lone_ms']:.1f} ms, interaction-wave wait {tm[14] / 2.4e6:.1f} ms geometry-wave wait "
           f"{tm[15] / 2.4e6:.1f} ms (s_memtime at 2.4 GHz)", flush=True)
+        for lo, what in ((16, "photons > 1e5 steps"), (22, "other photons")):
+            if tm[lo]:
+                n_, r_ = tm[lo], tm[lo + 1]
+                print(f"  lone geometry wave, {what}: {n_} steps, walk rounds/step {r_ / n_:.3f}, halved "
+                      f"{tm[lo + 5] / n_:.3f}; cycles/step: walk {tm[lo + 2] / n_:.0f} (per round "
+                      f"{tm[lo + 2] / max(r_, 1):.0f}) step_size+pack {tm[lo + 3] / n_:.0f} loop-rest "
+                      f"{tm[lo + 4] / n_:.0f}", flush=True)
