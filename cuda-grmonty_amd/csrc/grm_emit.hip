@@ -58,7 +58,7 @@ __device__ __forceinline__ uint32_t zone_count(const grm_emit_zone *zones, uint6
 /* counts of zones [z0, z0 + n) and their exclusive prefix sum off[0..n] (one workgroup; each
  * thread owns a contiguous chunk and recomputes its counts in the second pass instead of storing) */
 __global__ __launch_bounds__(SCAN_THREADS) void zone_count_scan(const grm_emit_zone *zones, uint64_t z0, uint64_t n,
-                                                                uint32_t k0, uint32_t k1, unsigned long long *off) {
+                                                                uint32_t k0, uint32_t k1, unsigned long long *off, unsigned long long *h_total) {
     __shared__ unsigned long long part[SCAN_THREADS];
     const uint64_t per = (n + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint64_t a = min(n, (uint64_t)threadIdx.x * per), b = min(n, a + per);
@@ -78,7 +78,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void zone_count_scan(const grm_emit_z
         off[q] = run;
         run += zone_count(zones, z0 + q, k0, k1);
     }
-    if (threadIdx.x == SCAN_THREADS - 1) off[n] = part[SCAN_THREADS - 1];
+    if (threadIdx.x == SCAN_THREADS - 1) {
+        off[n] = part[SCAN_THREADS - 1];
+        *h_total = part[SCAN_THREADS - 1]; /* host-mapped: no read-back copy */
+        __threadfence_system();
+    }
 }
 
 /* linear_interp_weight (harm_model.cpp:784-792); u = 1 exactly gives nu = nu_max: stay in the table */
@@ -189,13 +193,11 @@ int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t 
     };
     *n_out = 0;
     if (n_zones == 0) return 0;
-    hipLaunchKernelGGL(zone_count_scan, dim3(1), dim3(SCAN_THREADS), 0, s, E.zones, z0, n_zones, E.k0, E.k1, d_off);
-    if (!chk(hipGetLastError(), "zone_count_scan")) return -1;
-    /* h_total: pinned host word (a DMA transfer, no blit kernel competing for CUs) */
-    if (!chk(hipMemcpyAsync(h_total, d_off + n_zones, sizeof(*h_total), hipMemcpyDeviceToHost, s), "D2H") ||
-        !chk(hipStreamSynchronize(s), "sync"))
-        return -1;
-    const unsigned long long total = *h_total;
+    /* h_total: a host-mapped word the scan kernel writes itself (no copy kernel on the stream) */
+    hipLaunchKernelGGL(zone_count_scan, dim3(1), dim3(SCAN_THREADS), 0, s, E.zones, z0, n_zones, E.k0, E.k1, d_off,
+                       h_total);
+    if (!chk(hipGetLastError(), "zone_count_scan") || !chk(hipStreamSynchronize(s), "sync")) return -1;
+    const unsigned long long total = *(volatile unsigned long long *)h_total;
     if (total > *out_cap) {
         if (*out) (void)hipFree(*out);
         *out = nullptr;

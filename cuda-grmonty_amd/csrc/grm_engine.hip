@@ -791,8 +791,10 @@ __device__ __forceinline__ void unpack13(const double *d, double x[4], double k[
     e = d[12];
 }
 
-__global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C, unsigned long long n) {
-    if (blockIdx.x >= n) return;
+/* launched on lone_cap workgroups; the launch before handed over *C.lone_count photons */
+__global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
+    const unsigned long long n_handed = __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x >= n_handed || blockIdx.x >= C.lone_cap) return;
     const int wave = (int)(threadIdx.x >> 6);
     const int lane = (int)(threadIdx.x & 63);
     const LoneRec &R = C.lone[blockIdx.x];
@@ -1706,6 +1708,45 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     }
 }
 
+/* Stream-ordered control of the small device words, so that a pass needs no copy or fill
+ * (ROCclr blit) kernels: one workgroup sets the words a launch starts from (and, on a reset, the
+ * counters and the whole spectrum, grid-stride), then mirrors the counters and the small words into
+ * host-mapped memory, which the host reads after the stream synchronises. */
+struct CtlOp {
+    DevCounters *ctr;
+    unsigned long long *small; /* grm_engine::d_small */
+    double *spec;              /* zeroed on a reset (n_spec doubles) */
+    size_t n_spec;
+    DevCounters *h_ctr;        /* host-mapped mirrors (null: no mirror) */
+    unsigned long long *h_small;
+    unsigned long long val[8]; /* small[i] = val[i] for the bits of set */
+    unsigned set;
+    int reset, clear_abort;
+    unsigned long long max_tau_init_bits;
+};
+
+__global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
+    if (op.reset)
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < op.n_spec; i += (size_t)gridDim.x * 256)
+            op.spec[i] = 0.0;
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    if (op.reset) {
+        unsigned long long *c = reinterpret_cast<unsigned long long *>(op.ctr);
+        for (int i = 0; i < 16; ++i) c[i] = 0;
+        op.ctr->max_tau_bits = op.max_tau_init_bits;
+    }
+    if (op.clear_abort) op.ctr->abort = 0;
+    for (int i = 0; i < 8; ++i)
+        if ((op.set >> i) & 1u) op.small[i] = op.val[i];
+    if (op.h_ctr) {
+        const unsigned long long *c = reinterpret_cast<const unsigned long long *>(op.ctr);
+        unsigned long long *h = reinterpret_cast<unsigned long long *>(op.h_ctr);
+        for (int i = 0; i < 16; ++i) h[i] = c[i];
+        for (int i = 0; i < 8; ++i) op.h_small[i] = op.small[i];
+        __threadfence_system();
+    }
+}
+
 } /* namespace */
 
 /* ========================================================================= */
@@ -1714,7 +1755,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
 struct grm_engine {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     Params P{};
     double *d_zones = nullptr, *d_hot = nullptr, *d_k2 = nullptr;
     DevCounters *d_ctr = nullptr;
@@ -1755,13 +1796,12 @@ struct grm_engine {
     LoneRec *d_lone = nullptr;             /* photons handed over to lone_kernel */
     unsigned long long lone_cap = 0;
     int lone = 1;                          /* GRM_OPT_LONE */
-    /* pinned host staging for the per-pass small transfers: resets are H2D copies from pin->zero and
-     * readbacks land in pin->ctr / pin->word, all on the engine stream -- DMA engine transfers, where
-     * pageable copies and hipMemset would each need a blit/fill kernel, i.e. a free CU, which with
-     * other engines' transport blocks holding every CU can take seconds to get */
+    /* host-mapped control block: ctl_kernel mirrors the counters and the small words here (ctr,
+     * small) and the emission scan writes its total (word[4]); the host reads them after a stream
+     * synchronisation, so a pass runs without copy or fill kernels (see ctl_kernel) */
     struct Pinned {
-        unsigned long long zero[16384]; /* 128 KB >= the spectrum */
         DevCounters ctr;
+        unsigned long long small[8];
         unsigned long long word[8];
     } *pin = nullptr;
     /* device emission: zone table, emission tables, zone offsets, emitted photons */
@@ -1787,21 +1827,29 @@ bool hip_ok(grm_engine *e, hipError_t st, const char *what) {
         if (!hip_ok((e), (call), #call)) return -1;       \
     } while (0)
 
-/* stream-ordered small transfers through the pinned staging block (see grm_engine::pin) */
-int zero_async(grm_engine *e, void *dev, size_t bytes) {
-    while (bytes) {
-        const size_t k = std::min(bytes, sizeof(e->pin->zero));
-        HIPCHK(e, hipMemcpyAsync(dev, e->pin->zero, k, hipMemcpyHostToDevice, e->stream));
-        dev = static_cast<char *>(dev) + k;
-        bytes -= k;
+/* one ctl_kernel launch on the engine stream (op: the words to set; the mirror is always made) */
+int ctl(grm_engine *e, CtlOp op, bool sync) {
+    op.ctr = e->d_ctr;
+    op.small = e->d_small;
+    op.h_ctr = &e->pin->ctr;
+    op.h_small = e->pin->small;
+    unsigned blocks = 1;
+    if (op.reset) {
+        op.spec = reinterpret_cast<double *>(e->d_spec);
+        op.n_spec = sizeof(grm_spectrum_cell) / sizeof(double) * N_TH_BINS * N_E_BINS;
+        blocks = (unsigned)((op.n_spec + 255) / 256);
+        std::memcpy(&op.max_tau_init_bits, &e->max_tau_init, sizeof(double));
     }
+    hipLaunchKernelGGL(ctl_kernel, dim3(blocks), dim3(256), 0, e->stream, op);
+    HIPCHK(e, hipGetLastError());
+    if (sync) HIPCHK(e, hipStreamSynchronize(e->stream));
     return 0;
 }
 
+/* the device counters, through the host-mapped mirror */
 int read_counters(grm_engine *e, DevCounters &h) {
-    HIPCHK(e, hipMemcpyAsync(&e->pin->ctr, e->d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    h = e->pin->ctr;
+    if (ctl(e, CtlOp{}, true)) return -1;
+    h = e->pin->ctr; /* written by the device before the synchronisation returned */
     return 0;
 }
 
@@ -1932,20 +1980,21 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     int src = -1, dst = 0;
     unsigned long long n_pool = pos1 - pos0;
     for (int pass = 0; n_pool > 0; ++pass) {
-        if (zero_async(e, e->d_small, 3 * sizeof(unsigned long long))) return -1;
-        if (pass == 0 && pos0) { /* [0] pool head = first claim position */
-            e->pin->word[1] = pos0;
-            HIPCHK(e, hipMemcpyAsync(e->d_small, &e->pin->word[1], sizeof(unsigned long long), hipMemcpyHostToDevice,
-                                     e->stream));
-        }
-        if (pass == 0 && C.admit_n) { /* [4] in flight = 0, [5] end of the first warm-up batch */
+        /* the words this launch starts from: [0] pool head (the first claim position), [1 + dst] its
+         * overflow count (and that of the pool it drains), [4] in flight and [5] the end of the first
+         * warm-up batch, [7] hand-overs; the abort flag cleared */
+        CtlOp op{};
+        op.clear_abort = 1;
+        op.set = (1u << 0) | (1u << 1) | (1u << 2) | (1u << 7);
+        op.val[0] = pass == 0 ? pos0 : 0;
+        if (pass == 0 && C.admit_n) {
             const unsigned long long h = C.admit_h0;
-            e->pin->word[2] = 0;
-            e->pin->word[3] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
-                                                                        64ull, std::min(h, C.admit_lim - h)));
-            HIPCHK(e, hipMemcpyAsync(e->d_small + 4, &e->pin->word[2], 2 * sizeof(unsigned long long), hipMemcpyHostToDevice,
-                                     e->stream));
+            op.set |= (1u << 4) | (1u << 5);
+            op.val[4] = 0;
+            op.val[5] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
+                                                                    64ull, std::min(h, C.admit_lim - h)));
         }
+        if (ctl(e, op, false)) return -1;
         C.ovf = e->d_ovf[dst];
         C.ovf_count = e->d_small + 1 + dst;
         /* the per-wave record is kept of the first launch on the full grid (the bulk of a call) */
@@ -1959,40 +2008,33 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.pool_sh = 0;
             C.admit_n = 0;
         }
-        if (zero_async(e, &e->d_ctr->abort, sizeof(unsigned long long)) ||
-            zero_async(e, e->d_small + 7, sizeof(unsigned long long)))
-            return -1;
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
         hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
-        HIPCHK(e, hipMemcpyAsync(&e->pin->word[5], e->d_small + 7, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                 e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        /* the photons the launch handed over (a count on the device), one wave pair each; their
+         * children join this launch's overflow pool */
+        if (C.lone) {
+            HIPCHK(e, hipEventRecord(e->ev2, e->stream));
+            hipLaunchKernelGGL(lone_kernel, dim3((unsigned)e->lone_cap), dim3(128), 0, e->stream, e->P, C);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->ev3, e->stream));
+        }
+        DevCounters hp;
+        if (read_counters(e, hp)) return -1; /* synchronises */
         float ms = 0.f;
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
         ms_total += ms;
-        const unsigned long long n_lone = std::min<unsigned long long>(e->pin->word[5], e->lone_cap);
-        if (n_lone) {
-            /* the photons the launch handed over, one wave each; their children join this launch's
-             * overflow pool */
-            HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-            hipLaunchKernelGGL(lone_kernel, dim3((unsigned)n_lone), dim3(128), 0, e->stream, e->P, C, n_lone);
-            HIPCHK(e, hipGetLastError());
-            HIPCHK(e, hipEventRecord(e->ev1, e->stream));
-            HIPCHK(e, hipStreamSynchronize(e->stream));
+        const unsigned long long n_lone = std::min<unsigned long long>(e->pin->small[7], e->lone_cap);
+        if (C.lone) {
             float ms_l = 0.f;
-            HIPCHK(e, hipEventElapsedTime(&ms_l, e->ev0, e->ev1));
+            HIPCHK(e, hipEventElapsedTime(&ms_l, e->ev2, e->ev3));
             ms_total += ms_l;
             e->stats.lone_ms += ms_l;
             e->stats.n_lone += n_lone;
-            e->stats.n_launches++;
+            if (n_lone) e->stats.n_launches++;
         }
-        HIPCHK(e, hipMemcpyAsync(&e->pin->word[0], C.ovf_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                 e->stream));
-        DevCounters hp;
-        if (read_counters(e, hp)) return -1;
-        const unsigned long long cnt = e->pin->word[0];
+        const unsigned long long cnt = e->pin->small[1 + dst];
         if (ms > e->stats.max_launch_ms) { /* the dominant launch of this transport call */
             e->stats.max_launch_ms = ms;
             e->stats.max_launch_steps = hp.n_steps - steps_pass;
@@ -2065,16 +2107,10 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
 }
 
 int reset_counters(grm_engine *e) {
-    if (zero_async(e, e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS)) return -1;
-    DevCounters &h = e->pin->ctr;
-    std::memset(&h, 0, sizeof(h));
-    std::memcpy(&h.max_tau_bits, &e->max_tau_init, sizeof(double));
-    HIPCHK(e, hipMemcpyAsync(e->d_ctr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
-    if (zero_async(e, e->d_small, 4 * sizeof(unsigned long long)) ||
-        zero_async(e, e->d_small + 6, sizeof(unsigned long long)))
-        return -1;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    return 0;
+    CtlOp op{};
+    op.reset = 1;
+    op.set = 0xffu; /* every small word 0 */
+    return ctl(e, op, true);
 }
 
 } /* namespace */
@@ -2098,11 +2134,23 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     };
     if (!hip_ok(e, hipSetDevice(device), "hipSetDevice")) return fail();
     if (!hip_ok(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking), "stream")) return fail();
-    if (!hip_ok(e, hipEventCreate(&e->ev0), "event") || !hip_ok(e, hipEventCreate(&e->ev1), "event")) return fail();
-    if (!hip_ok(e, hipHostMalloc(reinterpret_cast<void **>(&e->pin), sizeof(grm_engine::Pinned), hipHostMallocDefault),
-                "pinned staging"))
+    if (!hip_ok(e, hipEventCreate(&e->ev0), "event") || !hip_ok(e, hipEventCreate(&e->ev1), "event") ||
+        !hip_ok(e, hipEventCreate(&e->ev2), "event") || !hip_ok(e, hipEventCreate(&e->ev3), "event"))
+        return fail();
+    if (!hip_ok(e, hipHostMalloc(reinterpret_cast<void **>(&e->pin), sizeof(grm_engine::Pinned),
+                                 hipHostMallocMapped | hipHostMallocCoherent),
+                "host-mapped control block"))
         return fail();
     std::memset(e->pin, 0, sizeof(grm_engine::Pinned));
+    {
+        /* the kernels write the block through the host pointer: it must be the device address too */
+        void *dp = nullptr;
+        if (!hip_ok(e, hipHostGetDevicePointer(&dp, e->pin, 0), "hipHostGetDevicePointer")) return fail();
+        if (dp != (void *)e->pin) {
+            e->err = "host-mapped control block: device address differs from the host address";
+            return fail();
+        }
+    }
     const size_t nz = (size_t)h->n[0] * h->n[1];
     std::vector<double> zones(nz * 8);
     for (size_t z = 0; z < nz; ++z)
@@ -2197,6 +2245,8 @@ void grm_engine_destroy(grm_engine *e) {
     if (e->comm) ncclCommDestroy(e->comm);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
+    if (e->ev2) hipEventDestroy(e->ev2);
+    if (e->ev3) hipEventDestroy(e->ev3);
     if (e->stream) hipStreamDestroy(e->stream);
     delete e;
 }

@@ -25,7 +25,7 @@ namespace {
 int g_verbose = 1; /* 0 warn, 1 info, 2 debug */
 
 template <typename... A>
-void info(const char *fmt, A... a) {
+__attribute__((format(printf, 1, 0))) void info(const char *fmt, A... a) {
     if (g_verbose >= 1) {
         std::fprintf(stderr, "[info] ");
         std::fprintf(stderr, fmt, a...);

@@ -21,6 +21,7 @@ top = dur[-k:]
 print(f"== track_kernel dispatches: {len(dur)}; the {k} longest (one dominant launch per pass): "
       f"mean {sum(top) / len(top):.1f} ms, min {top[0]:.1f} ms, max {top[-1]:.1f} ms")
 note = b["roofline"]["note"]
-print(f"== bench line under rocprof: value {b['value']:.4g} {b['unit']}, roofline achieved "
-      f"{b['roofline']['achieved']:.1f} GB/s, sustained {b['roofline'].get('achieved_sustained', 0):.1f} GB/s")
+rf = b["roofline"]
+print(f"== bench line under rocprof: value {b['value']:.4g} {b['unit']}, roofline ({rf['bound']}) achieved "
+      f"{rf['achieved']:.2f} {rf['unit']} of {rf['peak']} (frac {rf['frac']:.3f})")
 print(f"   {note}")
