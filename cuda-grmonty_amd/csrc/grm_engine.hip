@@ -215,7 +215,8 @@ __device__ __forceinline__ double bias_func(double den, double t_e, double w) {
  * LDS by the first active lane.  Slots: 0 child refill+sampling, 1 pool refill+init, 2 transport
  * trip, 3 loop total, 4 trips, 5 trips with a child sampled, 6 trips with an init, 7 bias refresh,
  * 8 phase-0 block, 9 push attempt, 10 restore / halving bookkeeping, 11 fluid gather,
- * 12 radiation + bias, 13 rest of the interaction; 15 = last stamp.  Never built into the product. */
+ * 12 radiation + bias, 13 rest of the interaction, 14 refill decision and claims (the loop top to
+ * the refill loads); 15 = last stamp.  Never built into the product. */
 #ifdef GRM_TIMING
 __shared__ unsigned long long g_tlds[GRM_BLOCK / 64][16];
 __device__ __forceinline__ void tstamp(int r) {
@@ -830,7 +831,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
 #ifdef GRM_TIMING
                     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
                     __builtin_amdgcn_s_sleep(1); /* the ring is full */
-                    if (lane == 0) atomicAdd(C.timing + 15, __builtin_amdgcn_s_memtime() - t0);
+                    if (lane == 0) atomicAdd(C.timing + 31, __builtin_amdgcn_s_memtime() - t0);
 #else
                     __builtin_amdgcn_s_sleep(1); /* the ring is full */
 #endif
@@ -968,7 +969,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
             while (__hip_atomic_load(&S0.tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != want)
                 __builtin_amdgcn_s_sleep(1);
 #ifdef GRM_TIMING
-            if (own) atomicAdd(C.timing + 14, __builtin_amdgcn_s_memtime() - tw0);
+            if (own) atomicAdd(C.timing + 30, __builtin_amdgcn_s_memtime() - tw0);
 #endif
         }
         const unsigned long long qj = base + (lane < LONE_BATCH ? lane : 0);
@@ -1553,6 +1554,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 if (k_child) TCOUNT(5);
                 if (k_pool) TCOUNT(6);
 #endif
+                TSTAMP(14);
                 bool has = false, ok = true;
                 if (!active && r < k_child) {
                     SReq R;
@@ -1778,7 +1780,7 @@ struct grm_engine {
     int grid_override = 0;
     double max_tau_init = 0.0;
     bool frozen_set = false;
-    int64_t warmup = 32768;  /* photons; -1 = lanes */
+    int64_t warmup = 4096;   /* photons; -1 = lanes (sweep: profiles/r02i_warmup_sweep.log) */
     int warmup_slack = 4;
     int refill_min = 2;      /* primaries: set-up is in the trip (phase 3), so refill early */
     int child_min = 8;       /* children: batch the divergent scattering sampling */

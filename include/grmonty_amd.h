@@ -137,8 +137,10 @@ enum {
     /* live-bias warm-up: until this many photons have been claimed since the last reset, they are
      * admitted in batches that double the history each time (the next batch once all but a
      * 2^-GRM_OPT_WARMUP_SLACK fraction of the history has ended), so the adaptive-bias counters
-     * evolve as in the serial reference (default 32768; -1 = one persistent grid's worth of lanes;
-     * 0 = off).  Tuned by the reference-semantics counters at 192^2 */
+     * evolve as in the serial reference (default 4096; -1 = one persistent grid's worth of lanes;
+     * 0 = off).  Tuned by the reference-semantics counters at 192^2: 0 doubles the
+     * recorded / scattered counts, 2048..32768 all land within the oracle's seed spread, and each
+     * doubling costs a batch barrier (~5-10 ms) per pass */
     GRM_OPT_WARMUP = 8,
     /* idle lanes a wavefront gathers before it takes emitted photons (1..64, default 2) */
     GRM_OPT_REFILL_MIN = 9,

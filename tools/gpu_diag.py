@@ -78,12 +78,12 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
     if inst:
         tot = max(tm[3], 1)
         names = {0: "child", 1: "init", 2: "trip-tail", 7: "bias", 8: "phase0", 9: "attempt", 10: "restore",
-                 11: "fluid", 12: "radiation", 13: "interact"}
+                 11: "fluid", 12: "radiation", 13: "interact", 14: "refill-decision"}
         print("  timing: " + " ".join(f"{v}={tm[k] / tot:.3f}" for k, v in names.items()) +
               f" | trips/wave {tm[4]} child-refills {tm[5] / max(tm[4], 1):.4f} pool-refills "
               f"{tm[6] / max(tm[4], 1):.4f} cycles/trip {tot / max(tm[4], 1):.0f} | lone kernel: {st['n_lone']} photons "
-          f"{st['lone_ms']:.1f} ms, interaction-wave wait {tm[14] / 2.4e6:.1f} ms geometry-wave wait "
-          f"{tm[15] / 2.4e6:.1f} ms (s_memtime at 2.4 GHz)", flush=True)
+          f"{st['lone_ms']:.1f} ms, interaction-wave wait {tm[30] / 2.4e6:.1f} ms geometry-wave wait "
+          f"{tm[31] / 2.4e6:.1f} ms (s_memtime at 2.4 GHz)", flush=True)
         for lo, what in ((16, "photons > 1e5 steps"), (22, "other photons")):
             if tm[lo]:
                 n_, r_ = tm[lo], tm[lo + 1]
