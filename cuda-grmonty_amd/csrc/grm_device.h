@@ -61,6 +61,32 @@ __device__ __forceinline__ double fratio_tol(double a, double b) {
     r = fma(r, fma(-b, r, 1.0), r);
     return fabs(a * r);
 }
+/* ---- natural logarithm ----
+ * ocml's log carries a double-double evaluation for < 0.5-ulp results (~90 VALU ops).  flog is the
+ * classic fdlibm reduction (x = 2^e m, m in [sqrt(1/2), sqrt(2)), s = (m-1)/(m+1), log m =
+ * 2 atanh s as f - f^2/2 + s (f^2/2 + R(s^2)), R a degree-14 minimax polynomial) in ~35 ops, < 1 ulp
+ * for positive normal x (tests/test_gpu_probes.py measures it against the host libm); every other x
+ * (0, subnormal, negative, inf, NaN) goes to ocml. */
+__device__ __forceinline__ double flog(double x) {
+    if (!(x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308)) return log(x);
+    double m = __builtin_amdgcn_frexp_mant(x); /* [0.5, 1) */
+    int e = __builtin_amdgcn_frexp_exp(x);
+    if (m < 0.70710678118654752440) {
+        m *= 2.0;
+        --e;
+    }
+    const double f = m - 1.0;
+    const double s = fdiv(f, 2.0 + f);
+    const double z = s * s, w = z * z;
+    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+    const double t2 = z * (6.666666666666735130e-01 +
+                           w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    const double r = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)e;
+    return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + r) + dk * 1.90821492927058770002e-10)) - f);
+}
+
 /* a / b for a kernel-argument divisor b with host reciprocal ib: one multiply (<= 1 ulp from a / b;
  * only grid / table coordinates go through it, whose interpolants are continuous across cells). */
 __device__ __forceinline__ double udiv(double a, double, double ib) { return a * ib; }
@@ -126,11 +152,11 @@ __device__ __forceinline__ double chi_sq(Rng &g, int dof) {
     double prod = uniform(g);
     const int m = dof >> 1;
     for (int i = 1; i < m; ++i) prod *= uniform(g);
-    double x = -2.0 * log(prod);
+    double x = -2.0 * flog(prod);
     if (dof & 1) {
         const double ua = uniform(g);
         const double ub = uniform(g);
-        const double z = sqrt(-2.0 * log(ua)) * cos(2.0 * kPi * ub);
+        const double z = sqrt(-2.0 * flog(ua)) * cospi(2.0 * ub); /* cos(2 pi ub), exact reduction */
         x += z * z;
     }
     return x;
@@ -669,7 +695,7 @@ __device__ __forceinline__ double alpha_inv_abs(const Params &P, double nu, doub
 __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k[4], const Fluid &F, double nu,
                                                  double &a_s, double &a_a) {
     const double theta_e = F.theta_e, n_e = F.n_e, b = F.b;
-    const double ln_te = log(theta_e);
+    const double ln_te = flog(theta_e);
     /* hotcross lookup index (hotcross.cpp:82-100) */
     const double w = nu * (HPL / (ME * CL * CL));
     const bool hc_thomson = w * theta_e < 1.0e-6;
@@ -679,7 +705,7 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
     const bool hc_table = !hc_thomson && !hc_kn && !hc_num;
     double fi = 0.0, fj = 0.0;
     if (hc_table) {
-        fi = udiv(log10(w) - P.hc_l_min_w, P.hc_d_l_w, P.hc_i_d_l_w);
+        fi = udiv(flog(w) * kLog10E - P.hc_l_min_w, P.hc_d_l_w, P.hc_i_d_l_w);
         fj = udiv(ln_te * kLog10E - P.hc_l_min_t, P.hc_d_l_t, P.hc_i_d_l_t);
     }
     const int i = hc_table ? (int)fi : 0, j = hc_table ? (int)fj : 0;
@@ -809,9 +835,8 @@ __device__ __forceinline__ void boost(const double v[4], const double u[4], doub
 
 __device__ __forceinline__ void sample_rand_dir(Rng &g, double &x, double &y, double &z) {
     z = uniform(g) * 2.0 - 1.0;
-    const double phi = uniform(g) * 2.0 * kPi;
     double s, c;
-    sincos(phi, &s, &c);
+    sincospi(2.0 * uniform(g), &s, &c); /* phi = 2 pi u: exact reduction */
     const double sq = sqrt(1.0 - z * z);
     x = sq * c;
     y = sq * s;
@@ -863,7 +888,7 @@ __device__ __forceinline__ void sample_electron(Rng &g, const double k[4], doubl
             sigma_kn = 1.0 - 2.0 * k_;
         else
             sigma_kn = (3.0 / (4.0 * k_ * k_)) * (2.0 + k_ * k_ * (1.0 + k_) / ((1.0 + 2.0 * k_) * (1.0 + 2.0 * k_)) +
-                                                  (k_ * k_ - 2.0 * k_ - 2.0) / (2.0 * k_) * log(1.0 + 2.0 * k_));
+                                                  (k_ * k_ - 2.0 * k_ - 2.0) / (2.0 * k_) * flog(1.0 + 2.0 * k_));
         x1 = uniform(g);
     } while (x1 >= sigma_kn);
     const double iv0 = 1.0 / sqrt(k[1] * k[1] + k[2] * k[2] + k[3] * k[3]);
@@ -877,9 +902,8 @@ __device__ __forceinline__ void sample_electron(Rng &g, const double k[4], doubl
     v1y *= iv1;
     v1z *= iv1;
     const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
-    const double phi = uniform(g) * 2.0 * kPi;
     double s_phi, c_phi;
-    sincos(phi, &s_phi, &c_phi);
+    sincospi(2.0 * uniform(g), &s_phi, &c_phi); /* phi = 2 pi u */
     const double c_th = mu, s_th = sqrt(1. - mu * mu);
     const double gb = gamma_e * beta_e;
     p[0] = gamma_e;
@@ -934,9 +958,8 @@ __device__ __forceinline__ void sample_scattered(Rng &g, const double k[4], doub
     v1y *= iv1;
     v1z *= iv1;
     const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
-    const double phi = 2.0 * kPi * uniform(g);
     double s_phi, c_phi;
-    sincos(phi, &s_phi, &c_phi);
+    sincospi(2.0 * uniform(g), &s_phi, &c_phi); /* phi = 2 pi u */
     p[1] = -p[1];
     p[2] = -p[2];
     p[3] = -p[3];

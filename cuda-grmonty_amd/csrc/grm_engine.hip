@@ -331,7 +331,7 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
         else
             ix2 = (int)((P.xe2 - x2) / P.th_dx2);
         if (ix2 >= 0 && ix2 < N_TH_BINS) {
-            i_e = (int)((log(e) - P.spec_l_e_0) / SPEC_D_L_E + 2.5) - 2;
+            i_e = (int)((flog(e) - P.spec_l_e_0) / SPEC_D_L_E + 2.5) - 2;
             if (i_e >= 0 && i_e < N_E_BINS) {
                 reason = 0;
                 atomicAdd(cnt + 0, 1ull);
@@ -1055,9 +1055,13 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
                 a_si = a_s;
                 a_ai = a_a;
                 bi = bf;
-                const double x1 = -log(uniform(rng));
+                /* x1 = -log u, settled without the logarithm when possible (as in transport_trip) */
+                const double u = uniform(rng);
+                const double bdt = bias * d_tau_scatt;
+                const bool may = bdt > (1.0 - u) * (1.0 - 0x1p-40);
+                const double x1 = may ? -flog(u) : 0.0;
                 const double wc = fdiv(w, bias);
-                if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) { /* :985 */
+                if (may && bdt > x1 && wc > WEIGHT_MIN) { /* :985 */
                     const double frac = fdiv(x1, bias * d_tau_scatt);
                     d_tau_abs *= frac;
                     if (d_tau_abs > 100) { /* absorbed before scattering */
@@ -1310,9 +1314,14 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             L.alpha_scatti() = a_s;
             L.alpha_absi() = a_a;
             L.bi() = bf;
-            const double x1 = -log(uniform(L.rng));
+            /* x1 = -log u (:983); the test bias * d_tau_scatt > x1 is settled without the logarithm
+             * when bias * d_tau_scatt <= (1 - u)(1 - 2^-40) <= -log u (margin for the log's rounding) */
+            const double u = uniform(L.rng);
+            const double bdt = bias * d_tau_scatt;
+            const bool may = bdt > (1.0 - u) * (1.0 - 0x1p-40);
+            const double x1 = may ? -flog(u) : 0.0;
             const double wc = fdiv(L.w, bias);
-            if (bias * d_tau_scatt > x1 && wc > WEIGHT_MIN) {
+            if (may && bdt > x1 && wc > WEIGHT_MIN) {
                 const double frac = fdiv(x1, bias * d_tau_scatt);
                 d_tau_abs *= frac;
                 if (d_tau_abs > 100) {

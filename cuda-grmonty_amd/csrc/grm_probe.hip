@@ -23,6 +23,7 @@
  * 16     w theta_e                                  sigma_hot (numerical quadrature fallback)
  * 17     x                                          e^x K_2(x)
  * 18     seed id dof                                chi^2 sample, ctr
+ * 19     x                                          flog(x), ocml log(x)
  */
 #include <hip/hip_runtime.h>
 
@@ -204,6 +205,10 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
     }
     case 16: store(o, 0, hotcross_num(a[0], a[1])); break;
     case 17: store(o, 0, k2_scaled(a[0])); break;
+    case 19:
+        store(o, 0, flog(a[0]));
+        store(o, 1, log(a[0]));
+        break;
     default: break;
     }
 }
@@ -213,7 +218,7 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
 extern "C" int grm_probe_impl(const Params &P, hipStream_t s, int which, const double *in, int in_stride, double *out,
                               int out_stride, size_t n, std::string &err) {
     if (n == 0) return 0;
-    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 18) {
+    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 19) {
         err = "grm_probe: bad arguments";
         return -1;
     }

@@ -272,3 +272,25 @@ def test_scattering_samplers(engine):
         if dev[i, 4] != ctr or not np.allclose(dev[i, :4], kp, rtol=1e-9, atol=1e-12 * np.max(np.abs(kp))):
             bad += 1
     assert bad <= 2
+
+
+def test_flog_accuracy(engine):
+    """flog (grm_device.h: fdlibm-style reduction, the hot path's natural log) vs the host libm:
+    <= 1 ulp on positive normal inputs over the whole range; 0, subnormal, negative, inf and NaN
+    take ocml's path and agree with numpy exactly."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([10.0 ** rng.uniform(-307, 308, 20000), 1.0 + rng.uniform(-1e-3, 1e-3, 5000),
+                        1.0 + rng.uniform(-1e-12, 1e-12, 2000), rng.uniform(0, 1, 5000),
+                        2.0 ** np.arange(-1022, 1024, dtype=np.float64), [1.0, np.nextafter(1.0, 2), np.nextafter(1.0, 0),
+                                                                         np.sqrt(0.5), 2.2250738585072014e-308]])
+    dev = engine.probe(19, x[:, None], 2)
+    ref = np.log(x)
+    ulp = np.abs(dev[:, 0] - ref) / np.spacing(np.abs(ref) + (ref == 0))
+    assert np.max(np.where(ref == 0, np.abs(dev[:, 0]) / 5e-324, ulp)) <= 1.0, np.max(ulp)
+    assert np.max(np.abs(dev[:, 1] - ref) / np.spacing(np.abs(ref) + (ref == 0))) <= 1.0  # ocml, for scale
+    special = np.array([0.0, -0.0, 5e-324, 1e-310, -1.0, np.inf, -np.inf, np.nan])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ref = np.log(special)
+    dev = engine.probe(19, special[:, None], 2)[:, 0]
+    np.testing.assert_array_equal(np.isnan(dev), np.isnan(ref))
+    np.testing.assert_array_equal(dev[~np.isnan(ref)], ref[~np.isnan(ref)])
