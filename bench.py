@@ -192,7 +192,7 @@ def main():
     if not args.dump:
         ensure_dump(path, args.grid, args.grid)
     t = time.time()
-    model = G.Model.load(path, photon_n=photon_n_job).init(threads)
+    model = G.Model.load(path, photon_n=photon_n_job).init(threads, device=local)
     t_init = time.time() - t
     shards = G.shard_zones(model.zone_weights(), world)
     z0, z1 = shards[rank]

@@ -97,6 +97,8 @@ SIGNATURES = {
     "grm_model_free": (None, [VP]),
     "grm_model_last_error": (C.c_char_p, []),
     "grm_model_init": (C.c_int, [VP, C.c_int]),
+    "grm_model_init_device": (C.c_int, [VP, C.c_int, C.c_int]),
+    "grm_model_table_ms": (C.c_double, [VP]),
     "grm_model_header": (None, [VP, C.POINTER(Header)]),
     "grm_model_units": (None, [VP, C.POINTER(Units)]),
     "grm_model_scalars": (None, [VP, DP]),
@@ -175,10 +177,21 @@ class Model:
         except Exception:
             pass
 
-    def init(self, n_threads: int = 0) -> "Model":
-        if self.L.grm_model_init(self.h, int(n_threads)) != 0:
+    def init(self, n_threads: int = 0, device=None) -> "Model":
+        """init() of the model (harm_model.cpp:234-240); device = a GPU index: the hotcross, K2 and
+        nint tables are built there (csrc/grm_tables.hip), the rest on the host."""
+        if device is None:
+            rc = self.L.grm_model_init(self.h, int(n_threads))
+        else:
+            rc = self.L.grm_model_init_device(self.h, int(n_threads), int(device))
+        if rc != 0:
             raise RuntimeError(self.L.grm_model_last_error().decode())
         return self
+
+    @property
+    def table_ms(self) -> float:
+        """GPU time (ms) of the device table builders of the last init(device=...)"""
+        return float(self.L.grm_model_table_ms(self.h))
 
     @property
     def header(self) -> Header:

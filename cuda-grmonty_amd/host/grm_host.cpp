@@ -287,6 +287,7 @@ struct grm_model {
     std::vector<double> fld[8];
     double bias_norm = 0, rh = 0, x1_min = 0, max_tau_scatt = 0, d_tau_k = 0;
     std::vector<double> hot, k2, ftab, weight, nint, dndlnu_max;
+    double table_ms = 0.0; /* GPU time of the device table builders (grm_model_init_device) */
     std::vector<double> gcov, gcon0, det; /* per zone: 16, 4 (row 0 of g^mu nu), 1 */
     bool inited = false;
     int n1() const { return hdr.n[0]; }
@@ -687,7 +688,25 @@ int grm_model_load(const char *path, int photon_n, double mass_unit, grm_model *
 void grm_model_free(grm_model *m) { delete m; }
 
 /* init(): harm_model.cpp:234-240 */
-int grm_model_init(grm_model *m, int n_threads) {
+/* library-internal device builders (csrc/grm_tables.hip) */
+int grm_tables_hot_k2_device(int device, const double c[13], const double *grid, double *hot, double *k2, float *ms,
+                             std::string &err);
+int grm_tables_nint_device(int device, const double c[13], const double *ftab, const double *weight, double *nint,
+                           double *dndlnu_max, float *ms, std::string &err);
+
+namespace {
+int model_init(grm_model *m, int n_threads, int device);
+}
+
+int grm_model_init(grm_model *m, int n_threads) { return model_init(m, n_threads, -1); }
+
+int grm_model_init_device(grm_model *m, int n_threads, int device) {
+    if (device < 0) return set_err("grm_model_init_device: device < 0");
+    return model_init(m, n_threads, device);
+}
+
+namespace {
+int model_init(grm_model *m, int n_threads, int device) {
     if (!m) return set_err("null model");
     if (n_threads < 1) n_threads = default_threads();
     const int n1 = m->n1(), n2 = m->n2();
@@ -706,8 +725,26 @@ int grm_model_init(grm_model *m, int n_threads) {
             m->det[z] = std::sqrt(std::abs(det4(&m->gcov[z * 16])));
         }
     });
+    /* device builders' constants (csrc/grm_tables.hip TableConsts) */
+    const grm_header &h = m->hdr;
+    const double nfac = h.dx[1] * h.dx[2] * h.dx[3] * m->units.l_unit * m->units.l_unit * m->units.l_unit * kSqrt2 *
+                        EE * EE * EE / (27.0 * ME * CL * CL) * (1.0 / HPL);
+    const double tc[13] = {K.hc_l_min_w, K.hc_d_l_w, K.hc_l_min_t, K.hc_d_l_t, K.jnu_l_min_t, K.jnu_d_l_t,
+                           K.jnu_l_min_k, K.jnu_d_l_k, K.l_nu_min, K.d_l_nu, K.l_b_min, K.d_l_b, nfac};
+    m->table_ms = 0.0;
     /* hotcross table (hotcross.cpp:60-79): one quadrature column per temperature */
     m->hot.assign((size_t)(HC_N_W + 1) * (HC_N_T + 1), 0.0);
+    m->ftab.assign(NSAMP + 1, 0.0);
+    m->k2.assign(NSAMP + 1, 0.0);
+    if (device >= 0) { /* hotcross and K2 on the GPU */
+        std::string err;
+        float ms = 0.f;
+        std::vector<double> grid(HC_N_W + 1 + HC_N_T + 1);
+        for (int ii = 0; ii <= HC_N_W; ++ii) grid[ii] = std::pow(10.0, K.hc_l_min_w + ii * K.hc_d_l_w);
+        for (int jj = 0; jj <= HC_N_T; ++jj) grid[HC_N_W + 1 + jj] = std::pow(10.0, K.hc_l_min_t + jj * K.hc_d_l_t);
+        if (grm_tables_hot_k2_device(device, tc, grid.data(), m->hot.data(), m->k2.data(), &ms, err)) return set_err(err);
+        m->table_ms += ms;
+    } else
     parallel_for(HC_N_T + 1, n_threads, [&](int jj) {
         const double l_t = K.hc_l_min_t + jj * K.hc_d_l_t;
         const double th = std::pow(10.0, l_t);
@@ -718,8 +755,6 @@ int grm_model_init(grm_model *m, int n_threads) {
         }
     });
     /* emission tables (jnu_mixed.cpp:57-73) */
-    m->ftab.assign(NSAMP + 1, 0.0);
-    m->k2.assign(NSAMP + 1, 0.0);
     try {
         parallel_for(NSAMP + 1, n_threads, [&](int q) {
             const double k = std::exp(q * K.jnu_d_l_k + K.jnu_l_min_k);
@@ -730,8 +765,10 @@ int grm_model_init(grm_model *m, int n_threads) {
                        std::exp(-std::pow(x, 1.0 / 3.0));
             };
             m->ftab[q] = std::log(4 * kPi * adaptive_gk61(integrand, 0, kPi / 2.0, 0.0, 1.0e-6, 1000));
-            const double tq = std::exp(q * K.jnu_d_l_t + K.jnu_l_min_t);
-            m->k2[q] = std::log(std::cyl_bessel_k(2, 1.0 / tq));
+            if (device < 0) {
+                const double tq = std::exp(q * K.jnu_d_l_t + K.jnu_l_min_t);
+                m->k2[q] = std::log(std::cyl_bessel_k(2, 1.0 / tq));
+            }
         });
     } catch (const std::exception &ex) {
         return set_err(ex.what());
@@ -739,7 +776,6 @@ int grm_model_init(grm_model *m, int n_threads) {
     /* weight table (:268-306): each frequency bin sums zones in reference order */
     std::vector<double> nu(NSAMP + 1);
     for (int q = 0; q <= NSAMP; ++q) nu[q] = std::exp(q * K.d_l_nu + K.l_nu_min);
-    const grm_header &h = m->hdr;
     const double s_fac = h.dx[1] * h.dx[2] * h.dx[3] * m->units.l_unit * m->units.l_unit * m->units.l_unit;
     std::vector<Fluid> zf(nz);
     std::vector<double> zfac(nz, 0.0);
@@ -764,8 +800,16 @@ int grm_model_init(grm_model *m, int n_threads) {
     /* nint table (:308-338) */
     m->nint.assign(NINT + 1, 0.0);
     m->dndlnu_max.assign(NINT + 1, 0.0);
-    const double nfac = h.dx[1] * h.dx[2] * h.dx[3] * m->units.l_unit * m->units.l_unit * m->units.l_unit * kSqrt2 *
-                        EE * EE * EE / (27.0 * ME * CL * CL) * (1.0 / HPL);
+    if (device >= 0) {
+        std::string err;
+        float ms = 0.f;
+        if (grm_tables_nint_device(device, tc, m->ftab.data(), m->weight.data(), m->nint.data(), m->dndlnu_max.data(),
+                                   &ms, err))
+            return set_err(err);
+        m->table_ms += ms;
+        m->inited = true;
+        return 0;
+    }
     parallel_for((NINT + 1 + 255) / 256, n_threads, [&](int blk) {
         for (int i = blk * 256; i < std::min(NINT + 1, (blk + 1) * 256); ++i) {
             double s = 0.0, dmax = 0.0;
@@ -784,6 +828,9 @@ int grm_model_init(grm_model *m, int n_threads) {
     m->inited = true;
     return 0;
 }
+} /* namespace */
+
+double grm_model_table_ms(const grm_model *m) { return m ? m->table_ms : 0.0; }
 
 void grm_model_header(const grm_model *m, grm_header *h) { *h = m->hdr; }
 void grm_model_units(const grm_model *m, grm_units *u) { *u = m->units; }

@@ -24,6 +24,10 @@ namespace {
 
 int g_verbose = 1; /* 0 warn, 1 info, 2 debug */
 
+void info(const char *msg) {
+    if (g_verbose >= 1) std::fprintf(stderr, "[info] %s\n", msg);
+}
+
 template <typename... A>
 __attribute__((format(printf, 1, 0))) void info(const char *fmt, A... a) {
     if (g_verbose >= 1) {

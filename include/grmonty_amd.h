@@ -224,6 +224,11 @@ void grm_model_free(grm_model *m);
 const char *grm_model_last_error(void);
 /* init(): geometry, hotcross, emission tables, weight, nint    harm_model.cpp:234-240 */
 int grm_model_init(grm_model *m, int n_threads);
+/* init() with the hotcross, K2 and nint / dndlnu_max tables built on GPU `device`
+ * (csrc/grm_tables.hip; the reference's GPU builder is hotcross_table.cu:35-65); the rest as
+ * grm_model_init.  grm_model_table_ms: GPU time of those builders (ms), 0 after grm_model_init. */
+int grm_model_init_device(grm_model *m, int n_threads, int device);
+double grm_model_table_ms(const grm_model *m);
 void grm_model_header(const grm_model *m, grm_header *h);
 void grm_model_units(const grm_model *m, grm_units *u);
 /* bias_norm, x1_min, max_tau_scatt (initial), d_tau_k, rh */
