@@ -87,6 +87,41 @@ __device__ __forceinline__ double flog(double x) {
     return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + r) + dk * 1.90821492927058770002e-10)) - f);
 }
 
+/* sin(pi x), cos(pi x) for |x| < 2^30 (every argument here is O(1)): exact reduction r = x - n/2,
+ * n = rint(2x) (|r| <= 1/4, the fma is exact), Taylor polynomials of sin(pi r)/r and cos(pi r) to
+ * degree 16 (truncation < 1e-18 on |r| <= 1/4), quadrant by the low bits of n.  ~32 ops against
+ * ocml's ~65 general-argument sincospi; <= 2 ulp (tests/test_gpu_probes.py, against mpmath). */
+__device__ __forceinline__ void fsincospi(double x, double &s, double &c) {
+    const double n = __builtin_rint(2.0 * x);
+    const double r = fma(n, -0.5, x);
+    const double t = r * r;
+    double ps = 7.952054001475513e-07;
+    ps = fma(ps, t, -2.1915353447830217e-05);
+    ps = fma(ps, t, 0.00046630280576761255);
+    ps = fma(ps, t, -0.0073704309457143504);
+    ps = fma(ps, t, 0.08214588661112823);
+    ps = fma(ps, t, -0.5992645293207921);
+    ps = fma(ps, t, 2.5501640398773455);
+    ps = fma(ps, t, -5.16771278004997);
+    const double sr = fma(r * t, ps, r * 3.141592653589793); /* r (pi + t P(t)) */
+    double pc = 4.303069587032947e-06;
+    pc = fma(pc, t, -0.0001046381049248457);
+    pc = fma(pc, t, 0.0019295743094039231);
+    pc = fma(pc, t, -0.02580689139001406);
+    pc = fma(pc, t, 0.2353306303588932);
+    pc = fma(pc, t, -1.3352627688545895);
+    pc = fma(pc, t, 4.0587121264167685);
+    pc = fma(pc, t, -4.934802200544679);
+    const double cr = fma(t, pc, 1.0);
+    const int q = (int)n;
+    const bool odd = (q & 1) != 0;
+    const double a = odd ? cr : sr, b = odd ? sr : cr;
+    /* sign flips as xor of the sign bit: s negated for q = 2, 3; c for q = 1, 2 (mod 4) */
+    const long long fs = (long long)(q & 2) << 62, fc = (long long)((q + 1) & 2) << 62;
+    s = __longlong_as_double(__double_as_longlong(a) ^ fs);
+    c = __longlong_as_double(__double_as_longlong(b) ^ fc);
+}
+
 /* a / b for a kernel-argument divisor b with host reciprocal ib: one multiply (<= 1 ulp from a / b;
  * only grid / table coordinates go through it, whose interpolants are continuous across cells). */
 __device__ __forceinline__ double udiv(double a, double, double ib) { return a * ib; }
@@ -156,7 +191,9 @@ __device__ __forceinline__ double chi_sq(Rng &g, int dof) {
     if (dof & 1) {
         const double ua = uniform(g);
         const double ub = uniform(g);
-        const double z = sqrt(-2.0 * flog(ua)) * cospi(2.0 * ub); /* cos(2 pi ub), exact reduction */
+        double sb, cb;
+        fsincospi(2.0 * ub, sb, cb); /* cos(2 pi ub), exact reduction */
+        const double z = sqrt(-2.0 * flog(ua)) * cb;
         x += z * z;
     }
     return x;
@@ -188,8 +225,8 @@ struct Trig {
  * one (agreement with sin/cos of the pi-multiplied argument to a few ulp) */
 __device__ __forceinline__ void trig_at(const Params &P, const double x[4], Trig &T) {
     T.r1 = exp(x[1]);
-    sincospi(2.0 * x[2], &T.s2x, &T.c2x);
-    sincospi(x[2] + ((1.0 - P.h_slope) / (2.0 * kPi)) * T.s2x, &T.sth, &T.cth);
+    fsincospi(2.0 * x[2], T.s2x, T.c2x);
+    fsincospi(x[2] + ((1.0 - P.h_slope) / (2.0 * kPi)) * T.s2x, T.sth, T.cth);
 }
 
 /* non-zero g_mu,nu of MKS Kerr + g^{00}, g^{01} (g^{02} = g^{03} = 0) */
@@ -836,7 +873,7 @@ __device__ __forceinline__ void boost(const double v[4], const double u[4], doub
 __device__ __forceinline__ void sample_rand_dir(Rng &g, double &x, double &y, double &z) {
     z = uniform(g) * 2.0 - 1.0;
     double s, c;
-    sincospi(2.0 * uniform(g), &s, &c); /* phi = 2 pi u: exact reduction */
+    fsincospi(2.0 * uniform(g), s, c); /* phi = 2 pi u: exact reduction */
     const double sq = sqrt(1.0 - z * z);
     x = sq * c;
     y = sq * s;
@@ -903,7 +940,7 @@ __device__ __forceinline__ void sample_electron(Rng &g, const double k[4], doubl
     v1z *= iv1;
     const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
     double s_phi, c_phi;
-    sincospi(2.0 * uniform(g), &s_phi, &c_phi); /* phi = 2 pi u */
+    fsincospi(2.0 * uniform(g), s_phi, c_phi); /* phi = 2 pi u */
     const double c_th = mu, s_th = sqrt(1. - mu * mu);
     const double gb = gamma_e * beta_e;
     p[0] = gamma_e;
@@ -959,7 +996,7 @@ __device__ __forceinline__ void sample_scattered(Rng &g, const double k[4], doub
     v1z *= iv1;
     const double v2x = v0y * v1z - v0z * v1y, v2y = v0z * v1x - v0x * v1z, v2z = v0x * v1y - v0y * v1x;
     double s_phi, c_phi;
-    sincospi(2.0 * uniform(g), &s_phi, &c_phi); /* phi = 2 pi u */
+    fsincospi(2.0 * uniform(g), s_phi, c_phi); /* phi = 2 pi u */
     p[1] = -p[1];
     p[2] = -p[2];
     p[3] = -p[3];

@@ -24,6 +24,7 @@
  * 17     x                                          e^x K_2(x)
  * 18     seed id dof                                chi^2 sample, ctr
  * 19     x                                          flog(x), ocml log(x)
+ * 20     x                                          fsincospi(x) s c, ocml sincospi(x) s c
  */
 #include <hip/hip_runtime.h>
 
@@ -209,6 +210,16 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
         store(o, 0, flog(a[0]));
         store(o, 1, log(a[0]));
         break;
+    case 20: {
+        double s0, c0, s1, c1;
+        fsincospi(a[0], s0, c0);
+        sincospi(a[0], &s1, &c1);
+        store(o, 0, s0);
+        store(o, 1, c0);
+        store(o, 2, s1);
+        store(o, 3, c1);
+        break;
+    }
     default: break;
     }
 }
@@ -218,7 +229,7 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
 extern "C" int grm_probe_impl(const Params &P, hipStream_t s, int which, const double *in, int in_stride, double *out,
                               int out_stride, size_t n, std::string &err) {
     if (n == 0) return 0;
-    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 19) {
+    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 20) {
         err = "grm_probe: bad arguments";
         return -1;
     }

@@ -7,19 +7,22 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 rev=$1; name=$2
 D="$R/cuda-grmonty_amd/build/rev_$name"
 rm -rf "$D"; mkdir -p "$D/csrc" "$D/include"
-for f in grm_engine.hip grm_probe.hip grm_emit.hip grm_device.h grm_emit.h; do
-  git -C "$R" show "$rev:cuda-grmonty_amd/csrc/$f" > "$D/csrc/$f"
+for f in grm_engine.hip grm_probe.hip grm_emit.hip grm_tables.hip grm_device.h grm_emit.h; do
+  git -C "$R" show "$rev:cuda-grmonty_amd/csrc/$f" > "$D/csrc/$f" 2>/dev/null || rm -f "$D/csrc/$f"
 done
 git -C "$R" show "$rev:include/grmonty_amd.h" > "$D/include/grmonty_amd.h"
 sed -i 's|"../../include/grmonty_amd.h"|"../include/grmonty_amd.h"|' "$D/csrc/"*.h "$D/csrc/"*.hip
 make -s -C "$R/cuda-grmonty_amd" build/grm_host.o
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -mllvm -disable-machine-licm"
 /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-sched-strategy=iterative-ilp $VFLAGS -c "$D/csrc/grm_engine.hip" -o "$D/grm_engine.o" &
-for f in grm_probe grm_emit; do
+objs="$D/grm_engine.o"
+for f in grm_probe grm_emit grm_tables; do
+  [ -f "$D/csrc/$f.hip" ] || continue
   /opt/rocm/bin/hipcc $FL -c "$D/csrc/$f.hip" -o "$D/$f.o" &
+  objs="$objs $D/$f.o"
 done
 wait
 mkdir -p "$R/cuda-grmonty_amd/variants"
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/cuda-grmonty_amd/variants/libgrmonty_amd_v$name.so" \
-  "$D/grm_engine.o" "$D/grm_probe.o" "$D/grm_emit.o" "$R/cuda-grmonty_amd/build/grm_host.o" -L/opt/rocm/lib -lrccl -lpthread
+  $objs "$R/cuda-grmonty_amd/build/grm_host.o" -L/opt/rocm/lib -lrccl -lpthread
 echo "built variants/libgrmonty_amd_v$name.so from $rev"
