@@ -295,42 +295,50 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
     const double irho2 = frcp(rho2), irho22 = irho2 * irho2, irho23 = irho22 * irho2;
     const double idthdx2 = frcp(dthdx2), irho23_dthdx2 = irho23 * idthdx2;
     const double fac1 = r2 - a2cth2, fac1_rho23 = fac1 * irho23;
-    const double fac2 = a2 + 2.0 * r2 + a2 * c2th;
     const double fac3 = a2 + r1 * (-2.0 + r1);
     const double i_r1rho23 = frcp(r1) * irho23;
-    /* fac2 = a^2 + 2 r^2 + a^2 cos(2 theta) = 2 rho^2: one reciprocal fewer (agreement to an ulp) */
-    const double i_sth = frcp(sth), ifac2 = 0.5 * irho2;
+    /* the reference's fac2 = a^2 + 2 r^2 + a^2 cos(2 theta) = 2 rho^2: written through rho^2 below */
+    const double i_sth = frcp(sth);
 
-    C.c[0][0] = 2.0 * r1 * fac1_rho23;
-    C.c[0][1] = r1 * (2.0 * r1 + rho2) * fac1_rho23;
-    C.c[0][2] = -a2 * r1 * s2th * dthdx2 * irho22;
-    C.c[0][3] = -2.0 * a * r1sth2 * fac1_rho23;
+    /* products shared between entries (reassociated: agreement with the reference's expressions to a
+     * few ulp, tests/test_gpu_probes.py::test_connection) */
+    const double r1f = r1 * fac1_rho23;                      /* r fac1 / rho^6 */
+    const double a2s2d = a2 * s2th * dthdx2 * irho22;         /* a^2 sin 2th dth/dx2 / rho^4 */
+    const double r1s2d = r1 * s2th * irho23_dthdx2;           /* r sin 2th / (rho^6 dth/dx2) */
+    const double d2r = dthdx22 * irho2;                       /* (dth/dx2)^2 / rho^2 */
+    const double fac3f = fac3 * fac1 * i_r1rho23;
+    const double arcd = a * r1 * cth * dthdx2 * i_sth * irho22;
+
+    C.c[0][0] = 2.0 * r1f;
+    C.c[0][1] = (2.0 * r1 + rho2) * r1f;
+    C.c[0][2] = -r1 * a2s2d;
+    C.c[0][3] = -2.0 * a * sth2 * r1f;
     C.c[0][4] = 2.0 * r2 * (r4 + r1 * fac1 - a4cth4) * irho23;
-    C.c[0][5] = -a2 * r2 * s2th * dthdx2 * irho22;
+    C.c[0][5] = -r2 * a2s2d;
     C.c[0][6] = a * r1 * (-r1 * (r3 + 2.0 * fac1) + a4cth4) * sth2 * irho23;
-    C.c[0][7] = -2.0 * r2 * dthdx22 * irho2;
-    C.c[0][8] = a3 * r1sth2 * s2th * dthdx2 * irho22;
+    C.c[0][7] = -2.0 * r2 * d2r;
+    C.c[0][8] = a * r1sth2 * a2s2d;
     C.c[0][9] = 2.0 * r1sth2 * (-r1 * rho22 + a2sth2 * fac1) * irho23;
 
-    C.c[1][0] = fac3 * fac1 * i_r1rho23;
+    C.c[1][0] = fac3f;
     C.c[1][1] = fac1 * (-2.0 * r1 + a2sth2) * irho23;
     C.c[1][2] = 0.0;
-    C.c[1][3] = -a * sth2 * fac3 * fac1 * i_r1rho23;
+    C.c[1][3] = -a * sth2 * fac3f;
     C.c[1][4] = (r4 * (-2.0 + r1) * (1.0 + r1) +
                  a2 * (a2 * r1 * (1.0 + 3.0 * r1) * cth4 + a4cth4 * cth2 + r3 * sth2 +
                        r1 * cth2 * (2.0 * r1 + 3.0 * r3 - a2sth2))) *
                 irho23;
-    C.c[1][5] = -a2 * dthdx2 * s2th * ifac2;
+    C.c[1][5] = -0.5 * rho2 * a2s2d; /* -a^2 dth/dx2 sin 2th / (2 rho^2) */
     C.c[1][6] = a * sth2 * (a4 * r1 * cth4 + r2 * (2.0 * r1 + r3 - a2sth2) + a2cth2 * (2.0 * r1 * (-1.0 + r2) + a2sth2)) *
                 irho23;
-    C.c[1][7] = -fac3 * dthdx22 * irho2;
+    C.c[1][7] = -fac3 * d2r;
     C.c[1][8] = 0.0;
     C.c[1][9] = -fac3 * sth2 * (r1 * rho22 - a2 * fac1 * sth2) * i_r1rho23;
 
-    C.c[2][0] = -a2 * r1 * s2th * irho23_dthdx2;
+    C.c[2][0] = -a2 * r1s2d;
     C.c[2][1] = r1 * C.c[2][0];
     C.c[2][2] = 0.0;
-    C.c[2][3] = a * r1 * (a2 + r2) * s2th * irho23_dthdx2;
+    C.c[2][3] = a * (a2 + r2) * r1s2d;
     C.c[2][4] = r2 * C.c[2][0];
     C.c[2][5] = r2 * irho2;
     C.c[2][6] = (a * r1 * cth * sth * (r3 * (2.0 + r1) + a2 * (2.0 * r1 * (1.0 + r1) * cth2 + a2 * cth4 + 2.0 * r1sth2))) *
@@ -341,14 +349,15 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
                 irho23_dthdx2;
 
     C.c[3][0] = a * fac1_rho23;
-    C.c[3][1] = r1 * C.c[3][0];
-    C.c[3][2] = -2.0 * a * r1 * cth * dthdx2 * i_sth * irho22;
+    C.c[3][1] = a * r1f;
+    C.c[3][2] = -2.0 * arcd;
     C.c[3][3] = -a2sth2 * fac1_rho23;
-    C.c[3][4] = a * r2 * fac1_rho23;
-    C.c[3][5] = -2 * a * r1 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * cth * dthdx2 * i_sth * (ifac2 * ifac2);
+    C.c[3][4] = a * r1 * r1f;
+    /* ifac2^2 = irho2^2 / 4 */
+    C.c[3][5] = -0.5 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * arcd;
     C.c[3][6] = r1 * (r1 * rho22 - a2sth2 * fac1) * irho23;
-    C.c[3][7] = -a * r1 * dthdx22 * irho2;
-    C.c[3][8] = dthdx2 * (0.25 * fac2 * fac2 * cth * i_sth + a2 * r1 * s2th) * irho22;
+    C.c[3][7] = -a * r1 * d2r;
+    C.c[3][8] = dthdx2 * (rho22 * cth * i_sth + a2 * r1 * s2th) * irho22; /* fac2^2 / 4 = rho^4 */
     C.c[3][9] = (-a * r1sth2 * rho22 + a3 * sth4 * fac1) * irho23;
 }
 
