@@ -392,10 +392,9 @@ __device__ __forceinline__ double step_size(const Params &P, const double x[4], 
 
 /* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
  * predicate of :1279 and the new energy e_1; leaves Trig and Gcov at the new x in T, G. */
-__device__ __forceinline__ bool push_attempt(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
-                                             double dl, double &e_1, Trig &T, Gcov &G) {
+/* push_attempt's halves: the half-step kick (x, k advanced, kp the predictor) ... */
+__device__ __forceinline__ void push_kick(double x[4], double k[4], const double dk[4], double dl, double kp[4]) {
     const double dl_2 = 0.5 * dl;
-    double kp[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const double d = dk[i] * dl_2;
@@ -403,9 +402,13 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
         kp[i] = k[i] + d;
         x[i] += k[i] * dl;
     }
-    trig_at(P, x, T);
-    Conn C;
-    connection(P, T, C);
+}
+
+/* ... and, with the connection at the new x, the corrector iterations and the energy check
+ * (g00, g01, g03 of the metric there) */
+__device__ __forceinline__ bool push_finish(const Conn &C, double k[4], double kp[4], double dk[4], double dl,
+                                            double e_0_s, double g00, double g01, double g03, double &e_1) {
+    const double dl_2 = 0.5 * dl;
     double err;
     int iter = 0;
     do {
@@ -421,12 +424,24 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
     } while (err > E_TOL && iter < MAX_ITER);
 #pragma unroll
     for (int i = 0; i < 4; ++i) k[i] = kp[i];
-    gcov_from_trig(P, T, G);
-    e_1 = -(k[0] * G.g00 + k[1] * G.g01 + k[3] * G.g03);
+    e_1 = -(k[0] * g00 + k[1] * g01 + k[3] * g03);
     /* |(e_1 - e_0_s) / e_0_s| > 1e-4 without the divide: same outcome for e_0_s = 0 (0/0 = NaN
      * fails neither test, x/0 = inf passes both) and NaN operands */
     const bool err_e = fabs(e_1 - e_0_s) > 1.0e-4 * fabs(e_0_s);
     return (err_e || err > E_TOL || isnan(err) || isinf(err));
+}
+
+/* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail
+ * predicate of :1279 and the new energy e_1; leaves Trig and Gcov at the new x in T, G. */
+__device__ __forceinline__ bool push_attempt(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
+                                             double dl, double &e_1, Trig &T, Gcov &G) {
+    double kp[4];
+    push_kick(x, k, dk, dl, kp);
+    trig_at(P, x, T);
+    Conn C;
+    connection(P, T, C);
+    gcov_from_trig(P, T, G);
+    return push_finish(C, k, kp, dk, dl, e_0_s, G.g00, G.g01, G.g03, e_1);
 }
 
 /* Per-lane spill slot for the push backup, laid out [component][lane] so that a wave's
