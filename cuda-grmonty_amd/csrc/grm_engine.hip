@@ -115,6 +115,7 @@ struct Ctl {
      * (~0 = no limit), *in_flight = photons started and not ended (children counted when pushed). */
     unsigned long long admit_n, admit_h0, admit_lim;
     int admit_slack;
+    unsigned long long admit_b0; /* first batch */
     unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     int lanes;
@@ -1527,7 +1528,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                     const unsigned long long h = C.admit_h0 + end;
                                     const unsigned long long next =
                                         end >= C.admit_n ? ~0ull
-                                                         : min(C.admit_n, end + max(64ull, min(h, C.admit_lim - h)));
+                                                         : min(C.admit_n, end + max(C.admit_b0, min(h, C.admit_lim - h)));
                                     atomicCAS(C.admit_end, end, next);
                                 }
                             }
@@ -1807,6 +1808,7 @@ struct grm_engine {
     LoneRec *d_lone = nullptr;             /* photons handed over to lone_kernel */
     unsigned long long lone_cap = 0;
     int lone = 1;                          /* GRM_OPT_LONE */
+    unsigned long long warmup_b0 = 64;     /* GRM_OPT_WARMUP_BATCH */
     /* host-mapped control block: ctl_kernel mirrors the counters and the small words here (ctr,
      * small) and the emission scan writes its total (word[4]); the host reads them after a stream
      * synchronisation, so a pass runs without copy or fill kernels (see ctl_kernel) */
@@ -1966,6 +1968,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.admit_h0 = e->history;
         C.admit_lim = limit;
         C.admit_slack = e->warmup_slack;
+        C.admit_b0 = e->warmup_b0;
     }
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
@@ -2003,7 +2006,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             op.set |= (1u << 4) | (1u << 5);
             op.val[4] = 0;
             op.val[5] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
-                                                                    64ull, std::min(h, C.admit_lim - h)));
+                                                                    C.admit_b0, std::min(h, C.admit_lim - h)));
         }
         if (ctl(e, op, false)) return -1;
         C.ovf = e->d_ovf[dst];
@@ -2289,6 +2292,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_CHILD_MIN: e->child_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_WARMUP_SLACK: e->warmup_slack = v < 0 ? 0 : (v > 30 ? 30 : (int)v); return 0;
     case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
+    case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }

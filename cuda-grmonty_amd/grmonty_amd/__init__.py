@@ -49,6 +49,7 @@ OPT_WATCHDOG_MS = 10
 OPT_CHILD_MIN = 11
 OPT_WARMUP_SLACK = 12
 OPT_LONE = 13
+OPT_WARMUP_BATCH = 14
 N_TH_BINS, N_E_BINS = 6, 200
 
 

@@ -154,10 +154,12 @@ enum {
     GRM_OPT_CHILD_MIN = 11,
     /* warm-up straggler tolerance, log2 (default 4: 1/16 of the history may still be in flight) */
     GRM_OPT_WARMUP_SLACK = 12,
-    /* 1 (default): a wave whose only work left is one photon hands it to the lone-photon kernel (one
-     * wave per photon, after the launch); 0: the lane loop keeps it; 2: every photon is handed over
+    /* 1 (default): a wave whose only work left is one photon hands it to the lone-photon kernel (two
+     * waves per photon, after the launch); 0: the lane loop keeps it; 2: every photon is handed over
      * at the top of its first step (tests of the lone-photon path) */
-    GRM_OPT_LONE = 13
+    GRM_OPT_LONE = 13,
+    /* photons of the first warm-up admission batch (default 64; later batches double the history) */
+    GRM_OPT_WARMUP_BATCH = 14
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

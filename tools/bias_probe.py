@@ -24,6 +24,7 @@ for mode, seed in [(md, sd) for md in modes for sd in seeds]:
     e.set_option(G.OPT_BIAS_MODE, 0)
     e.set_option(G.OPT_WARMUP, 32768)
     e.set_option(G.OPT_WARMUP_SLACK, 4)
+    e.set_option(G.OPT_WARMUP_BATCH, 64)
     if mode == "warmall":
         e.set_option(G.OPT_WARMUP, 10**9)
     elif mode.startswith("frozen"):
@@ -37,6 +38,8 @@ for mode, seed in [(md, sd) for md in modes for sd in seeds]:
         e.set_option(G.OPT_WARMUP, int(f[1]))
         if len(f) > 2:
             e.set_option(G.OPT_WARMUP_SLACK, int(f[2]))
+        if len(f) > 3:
+            e.set_option(G.OPT_WARMUP_BATCH, int(f[3]))
     t = time.time()
     p, n = e.emit(seed=seed)
     e.track_device(p, n)

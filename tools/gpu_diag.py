@@ -27,6 +27,9 @@ if os.environ.get("WARMUP"):
     e.set_option(G.OPT_WARMUP, int(os.environ["WARMUP"]))
     print(f"warmup {os.environ['WARMUP']}", flush=True)
 e.set_option(G.OPT_WATCHDOG_MS, int(os.environ.get("WATCHDOG_MS", "60000")))
+if os.environ.get("WARMUP_BATCH"):
+    e.set_option(G.OPT_WARMUP_BATCH, int(os.environ["WARMUP_BATCH"]))
+    print(f"warmup batch {os.environ['WARMUP_BATCH']}", flush=True)
 if os.environ.get("CHILD_MIN"):
     e.set_option(G.OPT_CHILD_MIN, int(os.environ["CHILD_MIN"]))
     print(f"child_min {os.environ['CHILD_MIN']}", flush=True)
