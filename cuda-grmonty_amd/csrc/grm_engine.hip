@@ -205,11 +205,13 @@ __device__ __forceinline__ double bias_den(const Params &P, const Ctl &C) {
 
 /* bias_func (harm_model.cpp:1391-1404), same expression and rounding as the reference */
 __device__ __forceinline__ double bias_func(double den, double t_e, double w) {
-    const double max = 0.5 * w / WEIGHT_MIN;
+    /* the constant divisions as multiplications by the rounded reciprocal (<= 1 ulp; an IEEE divide
+     * is 11 VALU ops and these run every step) */
+    const double max = w * (0.5 / WEIGHT_MIN);
     double bias = fdiv(100.0 * t_e * t_e, den);
     if (bias < TP_OVER_TE) bias = TP_OVER_TE;
     if (bias > max) bias = max;
-    return bias / TP_OVER_TE;
+    return bias * (1.0 / TP_OVER_TE);
 }
 
 /* Diagnostic build (-DGRM_TIMING): per-wave cycle attribution with s_memtime stamps, accumulated in
@@ -1073,7 +1075,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
                     d_tau_scatt *= frac;
                     const double d_tau = d_tau_abs + d_tau_scatt;
                     if (d_tau_abs < 1.0e-3)
-                        w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+                        w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
                     else
                         w *= exp(-d_tau);
                     /* photon_2 pushed to the scattering point (:1005-1010), by this wave */
@@ -1127,7 +1129,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
                     }
                     const double d_tau = d_tau_abs + d_tau_scatt;
                     if (d_tau < 1.0e-3)
-                        w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
+                        w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
                     else
                         w *= exp(-d_tau);
                 }
@@ -1332,7 +1334,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
                 d_tau_scatt *= frac;
                 const double d_tau = d_tau_abs + d_tau_scatt;
                 if (d_tau_abs < 1.0e-3)
-                    L.w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+                    L.w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
                 else
                     L.w *= exp(-d_tau);
                 /* re-push photon_2 by dl*frac to the scattering point (:1005), on later trips */
@@ -1353,7 +1355,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             }
             const double d_tau = d_tau_abs + d_tau_scatt;
             if (d_tau < 1.0e-3)
-                L.w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
+                L.w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
             else
                 L.w *= exp(-d_tau);
             L.tau_abs() += d_tau_abs;
