@@ -221,7 +221,7 @@ __device__ __forceinline__ double bias_func(double den, double t_e, double w) {
  * 12 radiation + bias, 13 rest of the interaction, 14 refill decision and claims (the loop top to
  * the refill loads); 15 = last stamp.  Never built into the product. */
 #ifdef GRM_TIMING
-__shared__ unsigned long long g_tlds[GRM_BLOCK / 64][16];
+__shared__ unsigned long long g_tlds[GRM_BLOCK / 64][24];
 __device__ __forceinline__ void tstamp(int r) {
     const unsigned long long t = __builtin_amdgcn_s_memtime();
     const unsigned long long ex = __ballot(1);
@@ -233,9 +233,19 @@ __device__ __forceinline__ void tstamp(int r) {
 }
 #define TSTAMP(r) tstamp(r)
 #define TCOUNT(r) do { if ((threadIdx.x & 63) == 0) g_tlds[threadIdx.x >> 6][r] += 1; } while (0)
+/* lane occupancy of a block: slot r counts executions, r + 1 the lanes in them (divergent callers) */
+#define TLANES(r, pred)                                                                            \
+    do {                                                                                           \
+        const unsigned long long b_ = __ballot(pred);                                              \
+        if (b_ && (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {               \
+            g_tlds[threadIdx.x >> 6][r] += 1;                                                      \
+            g_tlds[threadIdx.x >> 6][(r) + 1] += __popcll(b_);                                     \
+        }                                                                                          \
+    } while (0)
 #else
 #define TSTAMP(r) do { } while (0)
 #define TCOUNT(r) do { } while (0)
+#define TLANES(r, pred) do { } while (0)
 #endif
 
 /* stop_criterion (harm_model.cpp:1589-1616) */
@@ -1200,6 +1210,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
     Gcov G;
     ZoneFetch Z;
     bool have_tg = false;
+    TLANES(18, !walked && (setup || !(L.x[1] < P.xs1))); /* slots 18-19: push attempts */
     if (!walked && (setup || !(L.x[1] < P.xs1))) {
         if (L.depth > 0) {
             save_xkdk(bk, L);
@@ -1254,6 +1265,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         }
     }
     TSTAMP(10);
+    TLANES(16, setup || at_scatter || L.alpha_absi() > 0.0 || L.alpha_scatti() > 0.0 || L.fl_ne() > 0.0);
     if (setup || at_scatter || L.alpha_absi() > 0.0 || L.alpha_scatti() > 0.0 || L.fl_ne() > 0.0) {
         if (!have_tg) {
             trig_at(P, L.x, T);
@@ -1394,7 +1406,7 @@ __device__ void record_stuck(const Ctl &C, const Lane &L) {
 __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P, Ctl C) {
 #ifdef GRM_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    if ((threadIdx.x & 63) < 16) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
+    if ((threadIdx.x & 63) < 24) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
 #endif
     __shared__ double lds[2 * LDS_DOUBLES_PER_LANE * BLOCK];
     const Slot ph2{lds + threadIdx.x, BLOCK};
@@ -1680,6 +1692,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     if (lane_id == 0) {
         g_tlds[threadIdx.x >> 6][3] = __builtin_amdgcn_s_memtime() - t_start;
         for (int r = 0; r < 15; ++r) atomicAdd(C.timing + r, g_tlds[threadIdx.x >> 6][r]);
+        for (int r = 16; r < 24; ++r) atomicAdd(C.timing + 16 + r, g_tlds[threadIdx.x >> 6][r]);
     }
 #endif
     /* counters, then the workgroup's spectrum, to the global accumulators */
@@ -2222,8 +2235,8 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     P.zones = e->d_zones;
     P.hotcross = e->d_hot;
     P.k2 = e->d_k2;
-    if (!hip_ok(e, hipMalloc(&e->d_timing, 32 * sizeof(unsigned long long)), "timing") ||
-        !hip_ok(e, hipMemset(e->d_timing, 0, 32 * sizeof(unsigned long long)), "timing"))
+    if (!hip_ok(e, hipMalloc(&e->d_timing, 48 * sizeof(unsigned long long)), "timing") ||
+        !hip_ok(e, hipMemset(e->d_timing, 0, 48 * sizeof(unsigned long long)), "timing"))
         return fail();
     if (reset_counters(e)) return fail();
     *out = e;
@@ -2463,11 +2476,11 @@ int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm
     return 0;
 }
 
-int grm_engine_debug_timing(grm_engine *e, uint64_t out[32], int reset) {
+int grm_engine_debug_timing(grm_engine *e, uint64_t out[48], int reset) {
     if (!e || !out) return -1;
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, hipMemcpy(out, e->d_timing, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    if (reset) HIPCHK(e, hipMemset(e->d_timing, 0, 32 * sizeof(unsigned long long)));
+    HIPCHK(e, hipMemcpy(out, e->d_timing, 48 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(e, hipMemset(e->d_timing, 0, 48 * sizeof(unsigned long long)));
 #ifdef GRM_TIMING
     return 1;
 #else

@@ -362,7 +362,7 @@ class Engine:
         self._check(self.L.grm_engine_comm_init(self.h, buf, nranks, rank))
 
     def debug_timing(self, reset: bool = True):
-        out = (C.c_uint64 * 32)()
+        out = (C.c_uint64 * 48)()
         instrumented = self.L.grm_engine_debug_timing(self.h, out, 1 if reset else 0)
         return instrumented, list(out)
 

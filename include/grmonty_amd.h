@@ -193,9 +193,9 @@ int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap);
  * valid for grm_engine_track_device until the next upload or destroy. */
 int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm_init_photon **dev_out);
 
-/* diagnostic: per-region wave cycles of a -DGRM_TIMING build, 32 slots (returns 1 if the build
+/* diagnostic: per-region wave cycles of a -DGRM_TIMING build, 48 slots (returns 1 if the build
  * is instrumented, 0 if not; out[] then stays zero) */
-int grm_engine_debug_timing(grm_engine *e, uint64_t out[32], int reset);
+int grm_engine_debug_timing(grm_engine *e, uint64_t out[48], int reset);
 
 /* diagnostic: per-wave record of the last transport launch, 4 x u64 per wave: start and exit
  * (s_memrealtime, 100 MHz), loop trips, superphotons tracked.  out holds cap waves; returns the

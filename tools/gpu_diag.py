@@ -87,6 +87,9 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
               f"{tm[6] / max(tm[4], 1):.4f} cycles/trip {tot / max(tm[4], 1):.0f} | lone kernel: {st['n_lone']} photons "
           f"{st['lone_ms']:.1f} ms, interaction-wave wait {tm[30] / 2.4e6:.1f} ms geometry-wave wait "
           f"{tm[31] / 2.4e6:.1f} ms (s_memtime at 2.4 GHz)", flush=True)
+        if tm[34]:
+            print(f"  lane occupancy (track_kernel): push attempt {tm[35] / tm[34]:.1f} lanes in {tm[34]} executions, "
+                  f"fluid/radiation/interaction block {tm[33] / max(tm[32], 1):.1f} lanes in {tm[32]} executions", flush=True)
         for lo, what in ((16, "photons > 1e5 steps"), (22, "other photons")):
             if tm[lo]:
                 n_, r_ = tm[lo], tm[lo + 1]
