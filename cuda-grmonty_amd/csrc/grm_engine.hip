@@ -130,6 +130,14 @@ struct Ctl {
     LoneRec *lone;
     unsigned long long lone_cap, *lone_count;
     int lone_all;
+    /* early hand-over of long photons to the concurrent early_kernel (early_q null = off): a photon
+     * of >= early_steps steps at the top of a step; slots claimed by *early_tail, published by
+     * early_ready[slot] = early_tag; *wg_exit counts exited workgroups, the last sets *early_done;
+     * *early_live: set by early_kernel once it runs (no hand-over before, so none can strand) */
+    LoneRec *early_q;
+    unsigned long long *early_ready, early_cap, early_tag;
+    unsigned long long *early_tail, *early_head, *early_done, *wg_exit, *early_live;
+    int early_steps;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -781,8 +789,13 @@ struct alignas(16) LoneCtl {
     double rs[13];                /* restart state: photon_2 of the generation's first step */
     unsigned long long cons, req; /* steps consumed; restart request (generation << 32 | step) or LONE_STOP */
 };
-__shared__ LoneSlot s_ring[LONE_RING];
-__shared__ LoneCtl s_lctl;
+/* one photon's two-wave pipeline state (a geometry wave + an interaction wave) */
+struct LonePair {
+    LoneSlot ring[LONE_RING];
+    LoneCtl ctl;
+};
+constexpr int LONE_PAIRS = 4; /* pairs of the concurrent worker (early_kernel, 8 waves) */
+__shared__ LonePair s_pair[LONE_PAIRS];
 
 __device__ __forceinline__ void pack13(double *d, const double x[4], const double k[4], const double dk[4],
                                        double e) {
@@ -805,13 +818,138 @@ __device__ __forceinline__ void unpack13(const double *d, double x[4], double k[
     e = d[12];
 }
 
-/* launched on lone_cap workgroups; the launch before handed over *C.lone_count photons */
-__global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
-    const unsigned long long n_handed = __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (blockIdx.x >= n_handed || blockIdx.x >= C.lone_cap) return;
-    const int wave = (int)(threadIdx.x >> 6);
-    const int lane = (int)(threadIdx.x & 63);
-    const LoneRec &R = C.lone[blockIdx.x];
+/* The geometry wave of a pair (see above): runs photon after photon -- each begins as a restart
+ * request from the interaction wave -- until LONE_STOP. */
+__device__ void lone_geometry(const Params &P, const Ctl &C, int lane, LonePair &pr) {
+    unsigned gen = 0;
+    unsigned long long p = 0, cur = 0, cons = 0; /* cons: the last value read of pr.ctl.cons */
+    bool spec = false; /* speculate the halving depths on this step's push (the last one halved) */
+    double x[4], k[4], dk[4], e_0_s;
+    {
+        /* a photon starts as a restart (generation, step 0) from its hand-over state in rs */
+        unsigned long long r0;
+        while ((r0 = __hip_atomic_load(&pr.ctl.req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+            __builtin_amdgcn_s_sleep(2);
+        if (r0 == LONE_STOP) return;
+        cur = r0;
+        gen = (unsigned)(r0 >> 32);
+        p = r0 & 0xffffffffull;
+        cons = p;
+        unpack13(pr.ctl.rs, x, k, dk, e_0_s);
+    }
+#ifdef GRM_TIMING
+    unsigned long long g_last = __builtin_amdgcn_s_memtime();
+    unsigned long long tg[6] = {0, 0, 0, 0, 0, 0}; /* steps, rounds, walk, step size, rest, halved */
+#endif
+    while (true) {
+        if (p + 1 >= cons + LONE_RING) { /* the slot of step p and that of p - 1 must be consumed */
+            cons = __hip_atomic_load(&pr.ctl.cons, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (p + 1 >= cons + LONE_RING) {
+#ifdef GRM_TIMING
+                const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+                __builtin_amdgcn_s_sleep(1); /* the ring is full */
+                if (lane == 0) atomicAdd(C.timing + 31, __builtin_amdgcn_s_memtime() - t0);
+#else
+                __builtin_amdgcn_s_sleep(1); /* the ring is full */
+#endif
+                if (__hip_atomic_load(&pr.ctl.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == cur) continue;
+            }
+        }
+        /* the restart request (stop folded in as LONE_STOP): read once per step and looked at
+         * after the push, so that its LDS latency hides behind it; a step computed while a
+         * restart was pending is dropped (and one published just before a restart carries the
+         * old generation's tag, which the interaction wave skips) */
+        const unsigned long long req = __hip_atomic_load(&pr.ctl.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef GRM_TIMING
+        const unsigned long long g0 = __builtin_amdgcn_s_memtime();
+#endif
+        const double dl = step_size(P, x, k);
+#ifdef GRM_TIMING
+        const unsigned long long g1 = __builtin_amdgcn_s_memtime();
+#endif
+        /* Most steps pass their first attempt: then every lane makes that same attempt, the
+         * state stays identical over the wave and needs no broadcast.  A step that halves
+         * continues as a halving walk, and the next step speculates from the start. */
+        int rounds = 1;
+        {
+            if (!spec) {
+                bool fail = false;
+                if (!(x[1] < P.xs1)) {
+                    double xb[4], kb[4], dkb[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        xb[i] = x[i];
+                        kb[i] = k[i];
+                        dkb[i] = dk[i];
+                    }
+                    double e_1;
+                    Trig T;
+                    Gcov G;
+                    fail = push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
+                    if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            x[i] = xb[i];
+                            k[i] = kb[i];
+                            dk[i] = dkb[i];
+                        }
+                        rounds += walk_push(P, x, k, dk, e_0_s, dl, 1, 2u, lane, 0);
+                    } else {
+                        e_0_s = e_1;
+                    }
+                }
+                spec = fail;
+            } else {
+                rounds = walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, lane, 0);
+                spec = rounds > 1;
+            }
+        }
+        if (req != cur) {
+            if (req == LONE_STOP) {
+#ifdef GRM_TIMING
+                /* slots 16-21: photons of > 1e5 steps (the tail), 22-27: the others */
+                if (lane == 0)
+                    for (int r = 0; r < 6; ++r) atomicAdd(C.timing + (tg[0] > 100000 ? 16 : 22) + r, tg[r]);
+#endif
+                break;
+            }
+            /* restart from the scattering point (this step, if computed, is on the old geodesic) */
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); /* rs was written before req */
+            cur = req;
+            gen = (unsigned)(req >> 32);
+            p = req & 0xffffffffull;
+            cons = p; /* what the interaction wave has consumed when it requests a restart at p */
+            unpack13(pr.ctl.rs, x, k, dk, e_0_s);
+            spec = false;
+            continue;
+        }
+#ifdef GRM_TIMING
+        const unsigned long long g2 = __builtin_amdgcn_s_memtime();
+        tg[0] += 1;
+        tg[1] += (unsigned long long)rounds;
+        tg[2] += g2 - g1;
+        tg[3] += g1 - g0;
+        tg[4] += g0 - g_last;
+        tg[5] += spec ? 1ull : 0ull;
+        g_last = g2;
+#endif
+        if (lane == 0) {
+            LoneSlot &S = pr.ring[p % LONE_RING];
+            pack13(S.out, x, k, dk, e_0_s);
+            S.dl = dl;
+            /* LDS operations of a wave complete in order: the slot is written before its tag
+             * (a compiler barrier keeps the stores in program order; no wait for completion) */
+            __asm__ volatile("" ::: "memory");
+            __hip_atomic_store(&S.tag, ((unsigned long long)gen << 32) | (p + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        ++p;
+    }
+}
+
+/* The interaction wave of a pair: one handed-over photon, from its record to its end (the
+ * geometry wave is started on it with a restart request: generation gen + 1, step 0). */
+__device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, int lane, LonePair &pr, unsigned &gen_io) {
     double x[4], k[4], dk[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -820,129 +958,12 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
         dk[i] = R.dk[i];
     }
     double e_0_s = R.e_0_s;
-    if (threadIdx.x < 4) s_cnt[0][threadIdx.x] = 0;
-    if (threadIdx.x < LONE_RING) s_ring[threadIdx.x].tag = 0;
-    if (threadIdx.x == 0) {
-        s_lctl.cons = 0;
-        s_lctl.req = 0;
-        pack13(s_lctl.rs, x, k, dk, e_0_s); /* the state before step 0 */
+    unsigned gen = gen_io + 1;
+    if (lane == 0) {
+        pack13(pr.ctl.rs, x, k, dk, e_0_s); /* the state before step 0 */
+        pr.ctl.cons = 0;
+        __hip_atomic_store(&pr.ctl.req, (unsigned long long)gen << 32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __syncthreads();
-    if (wave == 1) {
-        /* ---- geometry wave ---- */
-        unsigned gen = 0;
-        unsigned long long p = 0, cur = 0, cons = 0; /* cons: the last value read of s_lctl.cons */
-        bool spec = false; /* speculate the halving depths on this step's push (the last one halved) */
-#ifdef GRM_TIMING
-        unsigned long long g_last = __builtin_amdgcn_s_memtime();
-        unsigned long long tg[6] = {0, 0, 0, 0, 0, 0}; /* steps, rounds, walk, step size, rest, halved */
-#endif
-        while (true) {
-            if (p + 1 >= cons + LONE_RING) { /* the slot of step p and that of p - 1 must be consumed */
-                cons = __hip_atomic_load(&s_lctl.cons, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (p + 1 >= cons + LONE_RING) {
-#ifdef GRM_TIMING
-                    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-                    __builtin_amdgcn_s_sleep(1); /* the ring is full */
-                    if (lane == 0) atomicAdd(C.timing + 31, __builtin_amdgcn_s_memtime() - t0);
-#else
-                    __builtin_amdgcn_s_sleep(1); /* the ring is full */
-#endif
-                    if (__hip_atomic_load(&s_lctl.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == cur) continue;
-                }
-            }
-            /* the restart request (stop folded in as LONE_STOP): read once per step and looked at
-             * after the push, so that its LDS latency hides behind it; a step computed while a
-             * restart was pending is dropped (and one published just before a restart carries the
-             * old generation's tag, which the interaction wave skips) */
-            const unsigned long long req = __hip_atomic_load(&s_lctl.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef GRM_TIMING
-            const unsigned long long g0 = __builtin_amdgcn_s_memtime();
-#endif
-            const double dl = step_size(P, x, k);
-#ifdef GRM_TIMING
-            const unsigned long long g1 = __builtin_amdgcn_s_memtime();
-#endif
-            /* Most steps pass their first attempt: then every lane makes that same attempt, the
-             * state stays identical over the wave and needs no broadcast.  A step that halves
-             * continues as a halving walk, and the next step speculates from the start. */
-            int rounds = 1;
-            {
-                if (!spec) {
-                    bool fail = false;
-                    if (!(x[1] < P.xs1)) {
-                        double xb[4], kb[4], dkb[4];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            xb[i] = x[i];
-                            kb[i] = k[i];
-                            dkb[i] = dk[i];
-                        }
-                        double e_1;
-                        Trig T;
-                        Gcov G;
-                        fail = push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
-                        if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) {
-                                x[i] = xb[i];
-                                k[i] = kb[i];
-                                dk[i] = dkb[i];
-                            }
-                            rounds += walk_push(P, x, k, dk, e_0_s, dl, 1, 2u, lane, 0);
-                        } else {
-                            e_0_s = e_1;
-                        }
-                    }
-                    spec = fail;
-                } else {
-                    rounds = walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, lane, 0);
-                    spec = rounds > 1;
-                }
-            }
-            if (req != cur) {
-                if (req == LONE_STOP) {
-#ifdef GRM_TIMING
-                    /* slots 16-21: photons of > 1e5 steps (the tail), 22-27: the others */
-                    if (lane == 0)
-                        for (int r = 0; r < 6; ++r) atomicAdd(C.timing + (tg[0] > 100000 ? 16 : 22) + r, tg[r]);
-#endif
-                    break;
-                }
-                /* restart from the scattering point (this step, if computed, is on the old geodesic) */
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); /* rs was written before req */
-                cur = req;
-                gen = (unsigned)(req >> 32);
-                p = req & 0xffffffffull;
-                unpack13(s_lctl.rs, x, k, dk, e_0_s);
-                spec = false;
-                continue;
-            }
-#ifdef GRM_TIMING
-            const unsigned long long g2 = __builtin_amdgcn_s_memtime();
-            tg[0] += 1;
-            tg[1] += (unsigned long long)rounds;
-            tg[2] += g2 - g1;
-            tg[3] += g1 - g0;
-            tg[4] += g0 - g_last;
-            tg[5] += spec ? 1ull : 0ull;
-            g_last = g2;
-#endif
-            if (lane == 0) {
-                LoneSlot &S = s_ring[p % LONE_RING];
-                pack13(S.out, x, k, dk, e_0_s);
-                S.dl = dl;
-                /* LDS operations of a wave complete in order: the slot is written before its tag
-                 * (a compiler barrier keeps the stores in program order; no wait for completion) */
-                __asm__ volatile("" ::: "memory");
-                __hip_atomic_store(&S.tag, ((unsigned long long)gen << 32) | (p + 1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            ++p;
-        }
-        return;
-    }
-    /* ---- interaction wave ---- */
     const bool own = lane == 0;
     const int rank = lane;
     double w = R.w;
@@ -961,7 +982,6 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
     unsigned long long steps = 0, children = 0;
     bool ended = false, abandoned = false;
     int reason = -1; /* ended without a record: trace reason */
-    unsigned gen = 0;
     unsigned long long gen_start = 0; /* the generation's first step */
     unsigned long long si = 0;        /* index of the next step */
     unsigned s = 0;            /* steps since the kernel start (refresh period) */
@@ -974,7 +994,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
          * values; a scattering discards the rest of the batch (the photon continues elsewhere). */
         const unsigned long long base = si;
         {
-            LoneSlot &S0 = s_ring[base % LONE_RING];
+            LoneSlot &S0 = pr.ring[base % LONE_RING];
             const unsigned long long want = ((unsigned long long)gen << 32) | (base + 1);
 #ifdef GRM_TIMING
             const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
@@ -986,7 +1006,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
 #endif
         }
         const unsigned long long qj = base + (lane < LONE_BATCH ? lane : 0);
-        const bool ready = lane < LONE_BATCH && __hip_atomic_load(&s_ring[qj % LONE_RING].tag, __ATOMIC_ACQUIRE,
+        const bool ready = lane < LONE_BATCH && __hip_atomic_load(&pr.ring[qj % LONE_RING].tag, __ATOMIC_ACQUIRE,
                                                                   __HIP_MEMORY_SCOPE_WORKGROUP) ==
                                                     (((unsigned long long)gen << 32) | (qj + 1));
         const unsigned long long rb = __ballot(ready);
@@ -994,7 +1014,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
         double l_ne, l_te, l_as = 0.0, l_aa = 0.0;
         int l_zero;
         {
-            const LoneSlot &Sj = s_ring[(base + (lane < nb ? lane : 0)) % LONE_RING];
+            const LoneSlot &Sj = pr.ring[(base + (lane < nb ? lane : 0)) % LONE_RING];
             double xj[4], kj[4], dkj[4], ej;
             unpack13(Sj.out, xj, kj, dkj, ej);
             Trig T;
@@ -1033,7 +1053,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
                 break;
             }
             /* photon_2, step size and push of this step: from the geometry wave */
-            const LoneSlot &S = s_ring[(base + bj) % LONE_RING];
+            const LoneSlot &S = pr.ring[(base + bj) % LONE_RING];
             double dkn[4], e_n;
             unpack13(S.out, x, k, dkn, e_n);
             const double dl = S.dl;
@@ -1091,7 +1111,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
                     /* photon_2 pushed to the scattering point (:1005-1010), by this wave */
                     double dk[4], e_0_s;
                     /* photon_2 of this step: the state after the step before, or the restart state */
-                    unpack13(base + bj == gen_start ? s_lctl.rs : s_ring[(base + bj - 1) % LONE_RING].out, x, k, dk,
+                    unpack13(base + bj == gen_start ? pr.ctl.rs : pr.ring[(base + bj - 1) % LONE_RING].out, x, k, dk,
                              e_0_s);
                     walk_push(P, x, k, dk, e_0_s, dl * frac, 0, 0u, rank, 0);
                     Trig T;
@@ -1126,8 +1146,8 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
                     ++gen;
                     gen_start = base + bj + 1;
                     if (own) {
-                        pack13(s_lctl.rs, x, k, dk, e_0_s);
-                        __hip_atomic_store(&s_lctl.req, ((unsigned long long)gen << 32) | (base + bj + 1),
+                        pack13(pr.ctl.rs, x, k, dk, e_0_s);
+                        __hip_atomic_store(&pr.ctl.req, ((unsigned long long)gen << 32) | (base + bj + 1),
                                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                     restart = true;
@@ -1153,11 +1173,11 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
                 break;
             }
             si = base + bj + 1;
-            if (own) __hip_atomic_store(&s_lctl.cons, si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (own) __hip_atomic_store(&pr.ctl.cons, si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (restart) break; /* the rest of the batch is on the old geodesic */
         }
     }
-    if (own) __hip_atomic_store(&s_lctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    gen_io = gen;
     if (own) {
         if (abandoned) {
             const unsigned long long slot = atomicAdd(C.stuck_count, 1ull);
@@ -1189,6 +1209,78 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
         atomicMax(&C.ctr->max_nstep, (unsigned long long)n_step);
         if (n_step > 100000) atomicAdd(&C.ctr->n_long, 1ull);
     }
+}
+
+/* launched on lone_cap workgroups; the launch before handed over *C.lone_count photons */
+__global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
+    const unsigned long long n_handed = __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x >= n_handed || blockIdx.x >= C.lone_cap) return;
+    const int wave = (int)(threadIdx.x >> 6);
+    const int lane = (int)(threadIdx.x & 63);
+    LonePair &pr = s_pair[0];
+    if (threadIdx.x < 8) s_cnt[threadIdx.x >> 2][threadIdx.x & 3] = 0;
+    if (threadIdx.x < LONE_RING) pr.ring[threadIdx.x].tag = 0;
+    if (threadIdx.x == 0) {
+        pr.ctl.cons = 0;
+        pr.ctl.req = 0;
+    }
+    __syncthreads();
+    if (wave == 1) {
+        lone_geometry(P, C, lane, pr);
+        return;
+    }
+    unsigned gen = 0;
+    lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen);
+    if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+/* Concurrent worker for long photons (one workgroup of LONE_PAIRS two-wave pairs on a second
+ * stream, beside the bulk launch): once it runs (early_live), a lane-loop photon that reaches early_steps steps is
+ * handed over at the top of a step into the early queue (slot claimed by early_tail, published by
+ * early_ready[slot] = early_tag); each pair's interaction wave claims slots in order (early_head),
+ * waits for them to be published and tracks them with its geometry wave.  It exits once the bulk
+ * launch has ended (early_done, set by its last workgroup) and every claimed slot is done.  Without
+ * it such a photon would advance one step per lane-loop trip (~7 us) until the bulk ends. */
+__global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ctl C) {
+    const int wave = (int)(threadIdx.x >> 6);
+    const int lane = (int)(threadIdx.x & 63);
+    LonePair &pr = s_pair[wave >> 1];
+    if (threadIdx.x < 4 * 2 * LONE_PAIRS) s_cnt[threadIdx.x >> 2][threadIdx.x & 3] = 0;
+    if (lane < LONE_RING) pr.ring[lane].tag = 0;
+    if (lane == 0) {
+        pr.ctl.cons = 0;
+        pr.ctl.req = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave & 1) {
+        lone_geometry(P, C, lane, pr);
+        return;
+    }
+    unsigned gen = 0;
+    while (true) {
+        unsigned long long slot = 0;
+        if (lane == 0) slot = atomicAdd(C.early_head, 1ull);
+        slot = (unsigned long long)__builtin_amdgcn_readfirstlane((int)slot); /* < 2^31 */
+        bool got = false;
+        while (true) {
+            if (slot < C.early_cap &&
+                __hip_atomic_load(C.early_ready + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == C.early_tag) {
+                got = true;
+                break;
+            }
+            if (__hip_atomic_load(C.early_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                /* the bulk launch has ended: every claimed hand-over is published, so a slot past the
+                 * claims (or past the queue) will never come */
+                const unsigned long long tail = __hip_atomic_load(C.early_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (slot >= tail || slot >= C.early_cap) break;
+            }
+            __builtin_amdgcn_s_sleep(64);
+        }
+        if (!got) break;
+        lone_interact(P, C, C.early_q[slot], lane, pr, gen);
+    }
+    if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 /* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
@@ -1636,6 +1728,20 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             continue;
         }
         wait_trips = 0;
+        /* a photon that has run early_steps steps goes to the concurrent early_kernel at the top of
+         * a step (one lane-loop trip is ~7 us per step for it, the pair ~1.8 us) */
+        if (C.early_q && !warm) {
+            const bool early = active && L.phase == 0 && L.n_step >= C.early_steps;
+            if (__ballot(early) && __hip_atomic_load(C.early_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && early) {
+                const unsigned long long slot = atomicAdd(C.early_tail, 1ull);
+                if (slot < C.early_cap) {
+                    export_lone(C.early_q + slot, L, cold);
+                    __threadfence();
+                    __hip_atomic_store(C.early_ready + slot, C.early_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    active = false;
+                }
+            }
+        }
         /* the tail: this wave's only work left is one photon -- hand it to the lone-photon kernel at
          * the top of a step (in the test mode GRM_OPT_LONE = 2: every photon at the top of its
          * first step); halving_walk finishes a push already in progress with the whole wave */
@@ -1733,6 +1839,14 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             wr[3] = w_tracked;
         }
     }
+    if (C.early_q) { /* the last workgroup out tells early_kernel that no hand-over will follow */
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(C.wg_exit, 1ull) == gridDim.x - 1)
+                __hip_atomic_store(C.early_done, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 /* Stream-ordered control of the small device words, so that a pass needs no copy or fill
@@ -1746,7 +1860,7 @@ struct CtlOp {
     size_t n_spec;
     DevCounters *h_ctr;        /* host-mapped mirrors (null: no mirror) */
     unsigned long long *h_small;
-    unsigned long long val[8]; /* small[i] = val[i] for the bits of set */
+    unsigned long long val[16]; /* small[i] = val[i] for the bits of set */
     unsigned set;
     int reset, clear_abort;
     unsigned long long max_tau_init_bits;
@@ -1763,13 +1877,13 @@ __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
         op.ctr->max_tau_bits = op.max_tau_init_bits;
     }
     if (op.clear_abort) op.ctr->abort = 0;
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 16; ++i)
         if ((op.set >> i) & 1u) op.small[i] = op.val[i];
     if (op.h_ctr) {
         const unsigned long long *c = reinterpret_cast<const unsigned long long *>(op.ctr);
         unsigned long long *h = reinterpret_cast<unsigned long long *>(op.h_ctr);
         for (int i = 0; i < 16; ++i) h[i] = c[i];
-        for (int i = 0; i < 8; ++i) op.h_small[i] = op.small[i];
+        for (int i = 0; i < 16; ++i) op.h_small[i] = op.small[i];
         __threadfence_system();
     }
 }
@@ -1823,13 +1937,22 @@ struct grm_engine {
     LoneRec *d_lone = nullptr;             /* photons handed over to lone_kernel */
     unsigned long long lone_cap = 0;
     int lone = 1;                          /* GRM_OPT_LONE */
+    /* early hand-over of long photons to early_kernel on a second stream (GRM_OPT_EARLY_STEPS) */
+    int early_steps = 5000;
+    static constexpr unsigned long long EARLY_CAP = 1024;
+    LoneRec *d_early = nullptr;
+    unsigned long long *d_early_ready = nullptr;
+    unsigned long long launch_seq = 0;
+    size_t waves_rows = 0; /* rows of d_waves the last recorded launch wrote */
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_pre = nullptr, ev_w = nullptr;
     unsigned long long warmup_b0 = 64;     /* GRM_OPT_WARMUP_BATCH */
     /* host-mapped control block: ctl_kernel mirrors the counters and the small words here (ctr,
      * small) and the emission scan writes its total (word[4]); the host reads them after a stream
      * synchronisation, so a pass runs without copy or fill kernels (see ctl_kernel) */
     struct Pinned {
         DevCounters ctr;
-        unsigned long long small[8];
+        unsigned long long small[16];
         unsigned long long word[8];
     } *pin = nullptr;
     /* device emission: zone table, emission tables, zone offsets, emitted photons */
@@ -2023,11 +2146,30 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             op.val[5] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
                                                                     C.admit_b0, std::min(h, C.admit_lim - h)));
         }
+        /* the main launch runs the early worker beside it: [8] early tail, [9] head, [10] done,
+         * [11] workgroups exited, [12] worker running */
+        const bool early = pass == 0 && C.pool_kind == 0 && e->early_steps > 0 && !C.lone_all && grid > 1;
+        if (early) op.set |= 0x1f00u;
         if (ctl(e, op, false)) return -1;
+        if (early) {
+            C.early_q = e->d_early;
+            C.early_ready = e->d_early_ready;
+            C.early_cap = grm_engine::EARLY_CAP;
+            C.early_tag = ++e->launch_seq;
+            C.early_tail = e->d_small + 8;
+            C.early_head = e->d_small + 9;
+            C.early_done = e->d_small + 10;
+            C.wg_exit = e->d_small + 11;
+            C.early_live = e->d_small + 12;
+            C.early_steps = e->early_steps;
+        } else {
+            C.early_q = nullptr;
+        }
         C.ovf = e->d_ovf[dst];
         C.ovf_count = e->d_small + 1 + dst;
         /* the per-wave record is kept of the first launch on the full grid (the bulk of a call) */
         C.waves = (pass == 0 && grid == e->grid) ? e->d_waves : nullptr;
+        if (C.waves) e->waves_rows = (size_t)grid * (BLOCK / 64);
         if (pass > 0) {
             C.pool = e->d_ovf[src];
             C.pool_kind = 1;
@@ -2037,7 +2179,18 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.pool_sh = 0;
             C.admit_n = 0;
         }
+        if (early) { /* after the control words are set; one workgroup, all of its pairs */
+            HIPCHK(e, hipEventRecord(e->ev_pre, e->stream));
+            HIPCHK(e, hipStreamWaitEvent(e->stream2, e->ev_pre, 0));
+            hipLaunchKernelGGL(early_kernel, dim3(1), dim3(64 * 2 * LONE_PAIRS), 0, e->stream2, e->P, C);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->ev_w, e->stream2));
+        }
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+        /* one workgroup per CU.  The early worker takes one CU too: workgroups are dealt to the XCDs
+         * round-robin, so with the worker's XCD full one bulk workgroup waits and starts (to find
+         * the pool empty) as the bulk drains -- 255 run either way, and a full grid needs no guess
+         * which XCD the worker lands on */
         hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
@@ -2049,12 +2202,14 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             HIPCHK(e, hipGetLastError());
             HIPCHK(e, hipEventRecord(e->ev3, e->stream));
         }
+        if (early) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_w, 0)); /* its photons' counters too */
         DevCounters hp;
         if (read_counters(e, hp)) return -1; /* synchronises */
         float ms = 0.f;
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
         ms_total += ms;
         const unsigned long long n_lone = std::min<unsigned long long>(e->pin->small[7], e->lone_cap);
+        if (early) e->stats.n_early += std::min<unsigned long long>(e->pin->small[8], grm_engine::EARLY_CAP);
         if (C.lone) {
             float ms_l = 0.f;
             HIPCHK(e, hipEventElapsedTime(&ms_l, e->ev2, e->ev3));
@@ -2138,7 +2293,7 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
 int reset_counters(grm_engine *e) {
     CtlOp op{};
     op.reset = 1;
-    op.set = 0xffu; /* every small word 0 */
+    op.set = 0xffffu; /* every small word 0 */
     return ctl(e, op, true);
 }
 
@@ -2164,7 +2319,13 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     if (!hip_ok(e, hipSetDevice(device), "hipSetDevice")) return fail();
     if (!hip_ok(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking), "stream")) return fail();
     if (!hip_ok(e, hipEventCreate(&e->ev0), "event") || !hip_ok(e, hipEventCreate(&e->ev1), "event") ||
-        !hip_ok(e, hipEventCreate(&e->ev2), "event") || !hip_ok(e, hipEventCreate(&e->ev3), "event"))
+        !hip_ok(e, hipEventCreate(&e->ev2), "event") || !hip_ok(e, hipEventCreate(&e->ev3), "event") ||
+        !hip_ok(e, hipEventCreateWithFlags(&e->ev_pre, hipEventDisableTiming), "event") ||
+        !hip_ok(e, hipEventCreateWithFlags(&e->ev_w, hipEventDisableTiming), "event") ||
+        !hip_ok(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking), "stream") ||
+        !hip_ok(e, hipMalloc(&e->d_early, grm_engine::EARLY_CAP * sizeof(LoneRec)), "early queue") ||
+        !hip_ok(e, hipMalloc(&e->d_early_ready, grm_engine::EARLY_CAP * sizeof(unsigned long long)), "early queue") ||
+        !hip_ok(e, hipMemset(e->d_early_ready, 0, grm_engine::EARLY_CAP * sizeof(unsigned long long)), "early queue"))
         return fail();
     if (!hip_ok(e, hipHostMalloc(reinterpret_cast<void **>(&e->pin), sizeof(grm_engine::Pinned),
                                  hipHostMallocMapped | hipHostMallocCoherent),
@@ -2190,9 +2351,9 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
         !hip_ok(e, hipMalloc(&e->d_k2, (GRM_N_E_SAMP + 1) * sizeof(double)), "k2") ||
         !hip_ok(e, hipMalloc(&e->d_ctr, sizeof(DevCounters)), "counters") ||
         !hip_ok(e, hipMalloc(&e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS), "spectrum") ||
-        !hip_ok(e, hipMalloc(&e->d_small, 8 * sizeof(unsigned long long)), "small") ||
+        !hip_ok(e, hipMalloc(&e->d_small, 16 * sizeof(unsigned long long)), "small") ||
         !hip_ok(e, hipMalloc(&e->d_stuck, STUCK_CAP * STUCK_WORDS * sizeof(double)), "stuck") ||
-        !hip_ok(e, hipMemset(e->d_small, 0, 8 * sizeof(unsigned long long)), "small"))
+        !hip_ok(e, hipMemset(e->d_small, 0, 16 * sizeof(unsigned long long)), "small"))
         return fail();
     if (!hip_ok(e, hipMemcpy(e->d_zones, zones.data(), nz * 8 * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
         !hip_ok(e, hipMemcpy(e->d_hot, hotcross, nhot * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
@@ -2276,6 +2437,11 @@ void grm_engine_destroy(grm_engine *e) {
     if (e->ev1) hipEventDestroy(e->ev1);
     if (e->ev2) hipEventDestroy(e->ev2);
     if (e->ev3) hipEventDestroy(e->ev3);
+    if (e->ev_pre) hipEventDestroy(e->ev_pre);
+    if (e->ev_w) hipEventDestroy(e->ev_w);
+    if (e->stream2) hipStreamDestroy(e->stream2);
+    hipFree(e->d_early);
+    hipFree(e->d_early_ready);
     if (e->stream) hipStreamDestroy(e->stream);
     delete e;
 }
@@ -2308,6 +2474,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_WARMUP_SLACK: e->warmup_slack = v < 0 ? 0 : (v > 30 ? 30 : (int)v); return 0;
     case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
+    case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }
@@ -2491,7 +2658,7 @@ int grm_engine_debug_timing(grm_engine *e, uint64_t out[48], int reset) {
 int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap) {
     if (!e || !e->d_waves) return -1;
     if (hipSetDevice(e->device) != hipSuccess) return -1;
-    const size_t n = e->lanes / 64;
+    const size_t n = std::min(e->lanes / 64, e->waves_rows);
     const size_t k = std::min(n, cap);
     if (k && out && hipMemcpy(out, e->d_waves, k * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;

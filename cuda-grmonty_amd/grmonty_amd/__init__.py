@@ -50,6 +50,7 @@ OPT_CHILD_MIN = 11
 OPT_WARMUP_SLACK = 12
 OPT_LONE = 13
 OPT_WARMUP_BATCH = 14
+OPT_EARLY_STEPS = 15
 N_TH_BINS, N_E_BINS = 6, 200
 
 
@@ -74,7 +75,8 @@ class Stats(C.Structure):
                 ("last_steps", C.c_uint64), ("last_emit_ms", C.c_double),
                 ("max_launch_ms", C.c_double), ("max_launch_steps", C.c_uint64),
                 ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64), ("n_abandoned", C.c_uint64),
-                ("n_nan_photons", C.c_uint64), ("n_lone", C.c_uint64), ("lone_ms", C.c_double)]
+                ("n_nan_photons", C.c_uint64), ("n_lone", C.c_uint64), ("lone_ms", C.c_double),
+                ("n_early", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -119,6 +119,7 @@ typedef struct grm_stats {
     uint64_t n_nan_photons;    /* superphotons ended at a NaN position since the last reset (see grm_engine.hip) */
     uint64_t n_lone;           /* photons handed over to the lone-photon kernel since the last reset */
     double lone_ms;            /* time in lone-photon kernel launches since the last reset */
+    uint64_t n_early;          /* long photons handed to the concurrent early worker since the last reset */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
@@ -159,7 +160,11 @@ enum {
      * at the top of its first step (tests of the lone-photon path) */
     GRM_OPT_LONE = 13,
     /* photons of the first warm-up admission batch (default 64; later batches double the history) */
-    GRM_OPT_WARMUP_BATCH = 14
+    GRM_OPT_WARMUP_BATCH = 14,
+    /* a photon of this many steps (default 5000; 0 = off) leaves the lane loop at the top of a step
+     * for a two-wave pair of the early worker, which runs beside the main transport launch on the CU
+     * that launch leaves free */
+    GRM_OPT_EARLY_STEPS = 15
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

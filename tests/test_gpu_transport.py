@@ -38,12 +38,14 @@ def setup(model64, oracle64):
     return G, O, sel, snap, eng
 
 
-@pytest.mark.parametrize("lone", [1, 2], ids=["lane-loop", "lone-kernel"])
+@pytest.mark.parametrize("lone", [1, 2, 3], ids=["lane-loop", "lone-kernel", "early-worker"])
 def test_photon_by_photon(setup, oracle64, lone):
-    """lone=2 hands every photon to the lone-photon kernel (one wave per photon, register state,
-    halving walks over the lanes) at the top of its first step: that path against the oracle"""
+    """lone=2 hands every photon to the lone-photon kernel (a two-wave pair per photon, halving walks
+    over the lanes) at the top of its first step; lone=3 hands every photon that reaches 40 steps to
+    the concurrent early worker (up to its queue's 1024): those paths against the oracle"""
     G, O, sel, snap, eng = setup
-    eng.set_option(G.OPT_LONE, lone)
+    eng.set_option(G.OPT_LONE, 1 if lone == 3 else lone)
+    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone == 3 else 5000)
     oracle64.reset()
     tr_o = oracle64.track(sel, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=snap["scatt"],
                           rec0=snap["rec"], max_tau0=snap["maxtau"], trace_cap=4_000_000)
@@ -63,8 +65,11 @@ def test_photon_by_photon(setup, oracle64, lone):
     eng.set_option(G.OPT_TRACE_CAP, 0)
     eng.set_option(G.OPT_BIAS_MODE, 0)
     eng.set_option(G.OPT_LONE, 1)
+    eng.set_option(G.OPT_EARLY_STEPS, 5000)
     if lone == 2:
         assert st["n_lone"] >= len(sel) // 2, st["n_lone"]
+    if lone == 3:
+        assert st["n_early"] >= 200, st["n_early"]
     assert st["n_dropped"] == 0
     assert st["n_primaries"] == len(sel)
     from parity_util import MIN_MATCH, check_spectrum_cells, trace_match
