@@ -947,20 +947,59 @@ __device__ void lone_geometry(const Params &P, const Ctl &C, int lane, LonePair 
     }
 }
 
+/* The draws of a lone photon come from a window of 64 consecutive Philox counters evaluated at once
+ * (lane i: counter wbase + i; the same block and bits as uniform(), so the same numbers in the same
+ * order): a serial draw is then two v_readlane instead of a 10-round Philox chain. */
+__device__ __forceinline__ double lone_draw(Rng &rng, double &win, uint32_t &wbase, int lane) {
+    if (rng.ctr - wbase >= 64u) { /* wave-uniform */
+        wbase = rng.ctr;
+        Rng g = rng;
+        g.ctr = wbase + (uint32_t)lane;
+        win = uniform(g);
+    }
+    const double u = bcast(win, (int)(rng.ctr - wbase));
+    ++rng.ctr;
+    return u;
+}
+
+/* stop_criterion (harm_model.cpp:1589-1616) with the windowed draws */
+__device__ __forceinline__ bool lone_stop(const Params &P, double x1, double &w, Rng &rng, double &win,
+                                          uint32_t &wbase, int lane) {
+    if (x1 < P.x1_min) return true;
+    if (x1 > P.x1_max) {
+        if (w < WEIGHT_MIN) {
+            if (lone_draw(rng, win, wbase, lane) <= 1.0 / ROULETTE)
+                w *= ROULETTE;
+            else
+                w = 0.0;
+        }
+        return true;
+    }
+    if (w < WEIGHT_MIN) {
+        if (lone_draw(rng, win, wbase, lane) <= 1.0 / ROULETTE) {
+            w *= ROULETTE;
+        } else {
+            w = 0.0;
+            return true;
+        }
+    }
+    return false;
+}
+
 /* The interaction wave of a pair: one handed-over photon, from its record to its end (the
  * geometry wave is started on it with a restart request: generation gen + 1, step 0). */
 __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, int lane, LonePair &pr, unsigned &gen_io) {
-    double x[4], k[4], dk[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        x[i] = R.x[i];
-        k[i] = R.k[i];
-        dk[i] = R.dk[i];
-    }
-    double e_0_s = R.e_0_s;
+    double x1 = R.x[1];
     unsigned gen = gen_io + 1;
     if (lane == 0) {
-        pack13(pr.ctl.rs, x, k, dk, e_0_s); /* the state before step 0 */
+        double x[4], k[4], dk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            x[i] = R.x[i];
+            k[i] = R.k[i];
+            dk[i] = R.dk[i];
+        }
+        pack13(pr.ctl.rs, x, k, dk, R.e_0_s); /* the state before step 0 */
         pr.ctl.cons = 0;
         __hip_atomic_store(&pr.ctl.req, (unsigned long long)gen << 32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -977,6 +1016,8 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
     rng.id = R.id;
     rng.ctr = R.ctr;
     rng.ctr_hi = 0;
+    double win = 0.0;
+    uint32_t wbase = rng.ctr - 64u; /* empty window */
     double bias_d = bias_den(P, C);
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long steps = 0, children = 0;
@@ -984,14 +1025,38 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
     int reason = -1; /* ended without a record: trace reason */
     unsigned long long gen_start = 0; /* the generation's first step */
     unsigned long long si = 0;        /* index of the next step */
-    unsigned s = 0;            /* steps since the kernel start (refresh period) */
+    /* the step whose end state is the photon's state (LONE_STOP: the restart state in rs) */
+    unsigned long long cur = LONE_STOP;
+    unsigned since = 0; /* steps since the last counter flush / bias refresh / watchdog look */
     bool done = false;
+#ifdef GRM_TIMING
+    unsigned long long ti[4] = {0, 0, 0, 0}; /* batches, steps in them, batch-evaluation cycles, serial cycles */
+#endif
     while (!done) {
         /* A batch: the consecutive steps the geometry wave has ready (at least one, at most
-         * LONE_BATCH).  Lane j evaluates the fluid and the absorption / scattering coefficients at
-         * the end point of step si + j at once -- the same code for every lane, and these depend on
-         * the geodesic only -- then the steps' interactions run in order, each taking its lane's
-         * values; a scattering discards the rest of the batch (the photon continues elsewhere). */
+         * LONE_BATCH).  Lane j evaluates step si + j at once: the fluid and the absorption /
+         * scattering coefficients at its end point (these depend on the geodesic only), and from
+         * them -- taking the previous step's coefficients from lane j - 1, as the serial recurrence
+         * has them whenever step j interacts -- its optical depths, the weight factor of a step
+         * without scattering and the weight-independent part of bias_func.  The steps then run in
+         * order, each taking its lane's values; a scattering discards the rest of the batch (the
+         * photon continues elsewhere). */
+        if (since >= REFRESH_TRIPS) { /* at a batch boundary, so that bias_d is fixed over a batch */
+            since = 0;
+            flush_counters(C);
+            if (!C.bias_frozen) bias_d = bias_den(P, C);
+            if (C.watchdog_ticks) {
+                bool stop = __hip_atomic_load(&C.ctr->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (!stop && __builtin_amdgcn_s_memrealtime() - rt_start > C.watchdog_ticks) {
+                    stop = true;
+                    if (own) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (stop) {
+                    abandoned = true;
+                    break;
+                }
+            }
+        }
         const unsigned long long base = si;
         {
             LoneSlot &S0 = pr.ring[base % LONE_RING];
@@ -1011,12 +1076,16 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
                                                     (((unsigned long long)gen << 32) | (qj + 1));
         const unsigned long long rb = __ballot(ready);
         const int nb = rb == ~0ull ? 64 : __ffsll((long long)~rb) - 1; /* leading run of ready steps (>= 1) */
-        double l_ne, l_te, l_as = 0.0, l_aa = 0.0;
+#ifdef GRM_TIMING
+        const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+#endif
+        double l_x1, l_ne, l_as = 0.0, l_aa = 0.0, l_dts, l_dta, l_b0, l_fac;
         int l_zero;
         {
             const LoneSlot &Sj = pr.ring[(base + (lane < nb ? lane : 0)) % LONE_RING];
             double xj[4], kj[4], dkj[4], ej;
             unpack13(Sj.out, xj, kj, dkj, ej);
+            const double dl = Sj.dl;
             Trig T;
             Gcov G;
             ZoneFetch Z;
@@ -1028,74 +1097,81 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
             const double nu = fluid_nu(kj, F);
             l_zero = (nu < 0.0 || F.n_e == 0.0) ? 1 : 0; /* bound_flag (:941-955) or nu < 0 */
             if (!l_zero) radiation_coeffs(P, kj, F, nu, l_as, l_aa);
+            l_x1 = xj[1];
             l_ne = F.n_e;
-            l_te = F.theta_e;
-        }
-        for (int bj = 0; bj < nb; ++bj) {
-            if ((++s & (REFRESH_TRIPS - 1)) == 0) {
-                flush_counters(C);
-                if (!C.bias_frozen) bias_d = bias_den(P, C);
-                if (C.watchdog_ticks) {
-                    bool stop = __hip_atomic_load(&C.ctr->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                    if (!stop && __builtin_amdgcn_s_memrealtime() - rt_start > C.watchdog_ticks) {
-                        stop = true;
-                        if (own) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    if (stop) {
-                        abandoned = done = true;
-                        break;
-                    }
-                }
+            /* the coefficients the step starts from: the step before's (lane j - 1), or the carried
+             * (the shuffles outside the conditional: with lane 0 masked off, lane 1 would read 0) */
+            const double up_as = __shfl_up(l_as, 1), up_aa = __shfl_up(l_aa, 1);
+            const double p_as = lane == 0 ? a_si : up_as, p_aa = lane == 0 ? a_ai : up_aa;
+            if (l_zero) {
+                l_dts = 0.5 * p_as * P.d_tau_k * dl;
+                l_dta = 0.5 * p_aa * P.d_tau_k * dl;
+                l_b0 = 0.0;
+            } else {
+                l_dts = 0.5 * (p_as + l_as) * P.d_tau_k * dl;
+                l_dta = 0.5 * (p_aa + l_aa) * P.d_tau_k * dl;
+                /* bias_func up to its weight cap (same operations) */
+                l_b0 = fdiv(100.0 * F.theta_e * F.theta_e, bias_d);
+                if (l_b0 < TP_OVER_TE) l_b0 = TP_OVER_TE;
             }
+            const double d_tau = l_dta + l_dts;
+            l_fac = d_tau < 1.0e-3 ? (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))))
+                                   : exp(-d_tau);
+        }
+#ifdef GRM_TIMING
+        const unsigned long long tb1 = __builtin_amdgcn_s_memtime();
+        ti[0] += 1;
+        ti[1] += (unsigned long long)nb;
+        ti[2] += tb1 - tb0;
+#endif
+        for (int bj = 0; bj < nb; ++bj) {
+            ++since;
             /* while (!stop_criterion(photon)) (:919) */
-            if (stop_criterion(P, x[1], w, rng)) {
+            if (lone_stop(P, x1, w, rng, win, wbase, lane)) {
                 ended = done = true;
                 break;
             }
             /* photon_2, step size and push of this step: from the geometry wave */
-            const LoneSlot &S = pr.ring[(base + bj) % LONE_RING];
-            double dkn[4], e_n;
-            unpack13(S.out, x, k, dkn, e_n);
-            const double dl = S.dl;
+            cur = base + bj;
+            x1 = bcast(l_x1, bj);
             ++steps;
-            if (stop_criterion(P, x[1], w, rng)) { /* :932-934 */
+            if (lone_stop(P, x1, w, rng, win, wbase, lane)) { /* :932-934 */
                 ended = done = true;
                 break;
             }
-            if (isnan(x[1])) { /* a NaN position is absorbing (see transport_trip) */
+            if (isnan(x1)) { /* a NaN position is absorbing (see transport_trip) */
                 if (own) atomicAdd(&C.ctr->n_nan, 1ull);
                 ended = done = true;
                 reason = 3;
                 break;
             }
-            bool restart = false;
             if (a_ai > 0.0 || a_si > 0.0 || fl_ne > 0.0) { /* :937 */
-                const double n_e = bcast(l_ne, bj), t_e = bcast(l_te, bj);
-                const double a_s = bcast(l_as, bj), a_a = bcast(l_aa, bj);
                 const bool zero = __builtin_amdgcn_readlane(l_zero, bj) != 0;
-                fl_ne = n_e;
-                const double bf = zero ? 0.0 : bias_func(bias_d, t_e, w);
-                double d_tau_scatt, d_tau_abs, bias;
-                if (zero) {
-                    d_tau_scatt = 0.5 * a_si * P.d_tau_k * dl;
-                    d_tau_abs = 0.5 * a_ai * P.d_tau_k * dl;
-                    bias = 0.0;
-                } else {
-                    d_tau_scatt = 0.5 * (a_si + a_s) * P.d_tau_k * dl;
-                    d_tau_abs = 0.5 * (a_ai + a_a) * P.d_tau_k * dl;
+                fl_ne = bcast(l_ne, bj);
+                double d_tau_scatt = bcast(l_dts, bj), d_tau_abs = bcast(l_dta, bj), bf = 0.0, bias = 0.0;
+                if (!zero) { /* bias_func's weight cap (:1391-1404) */
+                    const double max = w * (0.5 / WEIGHT_MIN);
+                    double b = bcast(l_b0, bj);
+                    if (b > max) b = max;
+                    bf = b * (1.0 / TP_OVER_TE);
                     bias = 0.5 * (bi + bf);
                 }
-                a_si = a_s;
-                a_ai = a_a;
+                a_si = bcast(l_as, bj);
+                a_ai = bcast(l_aa, bj);
                 bi = bf;
                 /* x1 = -log u, settled without the logarithm when possible (as in transport_trip) */
-                const double u = uniform(rng);
+                const double u = lone_draw(rng, win, wbase, lane);
                 const double bdt = bias * d_tau_scatt;
                 const bool may = bdt > (1.0 - u) * (1.0 - 0x1p-40);
-                const double x1 = may ? -flog(u) : 0.0;
-                const double wc = fdiv(w, bias);
-                if (may && bdt > x1 && wc > WEIGHT_MIN) { /* :985 */
-                    const double frac = fdiv(x1, bias * d_tau_scatt);
+                const double lx = may ? -flog(u) : 0.0;
+                bool scatter = may && bdt > lx;
+                double wc = 0.0;
+                if (scatter) { /* w / bias only when it decides (:985) */
+                    wc = fdiv(w, bias);
+                    scatter = wc > WEIGHT_MIN;
+                }
+                if (scatter) { /* :985 */
+                    const double frac = fdiv(lx, bias * d_tau_scatt);
                     d_tau_abs *= frac;
                     if (d_tau_abs > 100) { /* absorbed before scattering */
                         ended = done = true;
@@ -1109,11 +1185,11 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
                     else
                         w *= exp(-d_tau);
                     /* photon_2 pushed to the scattering point (:1005-1010), by this wave */
-                    double dk[4], e_0_s;
+                    double x[4], k[4], dk[4], e_0_s;
                     /* photon_2 of this step: the state after the step before, or the restart state */
                     unpack13(base + bj == gen_start ? pr.ctl.rs : pr.ring[(base + bj - 1) % LONE_RING].out, x, k, dk,
                              e_0_s);
-                    walk_push(P, x, k, dk, e_0_s, dl * frac, 0, 0u, rank, 0);
+                    walk_push(P, x, k, dk, e_0_s, pr.ring[(base + bj) % LONE_RING].dl * frac, 0, 0u, rank, 0);
                     Trig T;
                     Gcov G;
                     ZoneFetch Z;
@@ -1123,10 +1199,13 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
                     Fluid F;
                     fluid_from(P, x, G, Z, F);
                     fl_ne = F.n_e;
+                    x1 = x[1];
+                    cur = LONE_STOP; /* the state is the restart state from here on */
                     if (F.n_e > 0.0 && (k[0] > 1.0e5 || k[0] < 0.0 || isnan(k[0]) || isnan(k[1]) || isnan(k[3]))) {
                         /* scatter_super_photon's parent-side check (:1076-1081, :1018-1021) */
                         k[0] = fabs(k[0]);
                         w = 0.0;
+                        if (own) pack13(pr.ctl.rs, x, k, dk, e_0_s);
                         ended = done = true;
                         reason = 2;
                         break;
@@ -1150,18 +1229,26 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
                         __hip_atomic_store(&pr.ctl.req, ((unsigned long long)gen << 32) | (base + bj + 1),
                                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    restart = true;
+                    /* the end of the step here, and the end of the batch (the rest of it is on the old
+                     * geodesic): the batch's lane values are dead on this path */
+                    tau_abs += d_tau_abs;
+                    tau_scatt += d_tau_scatt;
+                    ++n_step; /* :1058-1063 */
+                    if (n_step > MAX_N_STEP) {
+                        ended = done = true;
+                        reason = 3;
+                        break;
+                    }
+                    si = base + bj + 1;
+                    if (own) __hip_atomic_store(&pr.ctl.cons, si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
                 } else {
                     if (d_tau_abs > 100) { /* absorbed */
                         ended = done = true;
                         reason = 2;
                         break;
                     }
-                    const double d_tau = d_tau_abs + d_tau_scatt;
-                    if (d_tau < 1.0e-3)
-                        w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
-                    else
-                        w *= exp(-d_tau);
+                    w *= bcast(l_fac, bj);
                 }
                 tau_abs += d_tau_abs;
                 tau_scatt += d_tau_scatt;
@@ -1174,11 +1261,22 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
             }
             si = base + bj + 1;
             if (own) __hip_atomic_store(&pr.ctl.cons, si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (restart) break; /* the rest of the batch is on the old geodesic */
         }
+#ifdef GRM_TIMING
+        ti[3] += __builtin_amdgcn_s_memtime() - tb1;
+#endif
     }
+#ifdef GRM_TIMING
+    /* slots 36-39: photons of > 1e5 steps, 40-43: the others */
+    if (own)
+        for (int r = 0; r < 4; ++r) atomicAdd(C.timing + (steps > 100000 ? 36 : 40) + r, ti[r]);
+#endif
     gen_io = gen;
     if (own) {
+        /* the photon's state: the end of step cur (its ring slot is not overwritten before this wave
+         * consumes the step after it), or the restart state */
+        double x[4], k[4], dk[4], e_0_s;
+        unpack13(cur == LONE_STOP ? pr.ctl.rs : pr.ring[cur % LONE_RING].out, x, k, dk, e_0_s);
         if (abandoned) {
             const unsigned long long slot = atomicAdd(C.stuck_count, 1ull);
             if (slot < C.stuck_cap) {

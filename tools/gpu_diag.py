@@ -93,6 +93,11 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
         if tm[34]:
             print(f"  lane occupancy (track_kernel): push attempt {tm[35] / tm[34]:.1f} lanes in {tm[34]} executions, "
                   f"fluid/radiation/interaction block {tm[33] / max(tm[32], 1):.1f} lanes in {tm[32]} executions", flush=True)
+        for lo, what in ((36, "photons > 1e5 steps"), (40, "other photons")):
+            if tm[lo]:
+                print(f"  lone interaction wave, {what}: {tm[lo]} batches of {tm[lo + 1] / tm[lo]:.2f} steps; cycles: "
+                      f"batch evaluation {tm[lo + 2] / tm[lo]:.0f} per batch, serial {tm[lo + 3] / tm[lo + 1]:.0f} per "
+                      f"step, total {(tm[lo + 2] + tm[lo + 3]) / tm[lo + 1]:.0f} per step", flush=True)
         for lo, what in ((16, "photons > 1e5 steps"), (22, "other photons")):
             if tm[lo]:
                 n_, r_ = tm[lo], tm[lo + 1]
