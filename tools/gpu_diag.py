@@ -30,6 +30,9 @@ e.set_option(G.OPT_WATCHDOG_MS, int(os.environ.get("WATCHDOG_MS", "60000")))
 if os.environ.get("EARLY_STEPS"):
     e.set_option(G.OPT_EARLY_STEPS, int(os.environ["EARLY_STEPS"]))
     print(f"early steps {os.environ['EARLY_STEPS']}", flush=True)
+if os.environ.get("SLACK"):
+    e.set_option(G.OPT_WARMUP_SLACK, int(os.environ["SLACK"]))
+    print(f"warmup slack {os.environ['SLACK']}", flush=True)
 if os.environ.get("WARMUP_BATCH"):
     e.set_option(G.OPT_WARMUP_BATCH, int(os.environ["WARMUP_BATCH"]))
     print(f"warmup batch {os.environ['WARMUP_BATCH']}", flush=True)
