@@ -133,10 +133,12 @@ struct Ctl {
     /* early hand-over of long photons to the concurrent early_kernel (early_q null = off): a photon
      * of >= early_steps steps at the top of a step; slots claimed by *early_tail, published by
      * early_ready[slot] = early_tag; *wg_exit counts exited workgroups, the last sets *early_done;
-     * *early_live: set by early_kernel once it runs (no hand-over before, so none can strand) */
+     * *early_live: 1 once early_kernel runs (no hand-over before, so none can strand), 2 when it
+     * closed the queue because the bulk launch had not started (kernels serialised, e.g. under a
+     * counter profiler); *bulk_live: set by every bulk workgroup as it starts */
     LoneRec *early_q;
     unsigned long long *early_ready, early_cap, early_tag;
-    unsigned long long *early_tail, *early_head, *early_done, *wg_exit, *early_live;
+    unsigned long long *early_tail, *early_head, *early_done, *wg_exit, *early_live, *bulk_live;
     int early_steps;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
@@ -795,6 +797,9 @@ struct LonePair {
     LoneCtl ctl;
 };
 constexpr int LONE_PAIRS = 4; /* pairs of the concurrent worker (early_kernel, 8 waves) */
+/* early_kernel waits this long (s_memrealtime, 100 MHz) for the bulk launch to start before it
+ * takes the launches for serialised and leaves */
+constexpr unsigned long long EARLY_ALONE_TICKS = 100000; /* 1 ms */
 __shared__ LonePair s_pair[LONE_PAIRS];
 
 __device__ __forceinline__ void pack13(double *d, const double x[4], const double k[4], const double dk[4],
@@ -1350,7 +1355,8 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
         pr.ctl.req = 0;
     }
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
     if (wave & 1) {
         lone_geometry(P, C, lane, pr);
         return;
@@ -1372,6 +1378,18 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
                  * claims (or past the queue) will never come */
                 const unsigned long long tail = __hip_atomic_load(C.early_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 if (slot >= tail || slot >= C.early_cap) break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - rt_start > EARLY_ALONE_TICKS &&
+                __builtin_amdgcn_readfirstlane(
+                    (int)__hip_atomic_load(C.bulk_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                /* no bulk workgroup has started: the launches are serialised and this one runs first.
+                 * Close the queue, then leave unless a bulk workgroup started meanwhile (then reopen
+                 * it: a workgroup that read 1 after starting is seen here by the store-load order) */
+                if (lane == 0) __hip_atomic_store(C.early_live, 2ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane(
+                        (int)__hip_atomic_load(C.bulk_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+                    break;
+                if (lane == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
             }
             __builtin_amdgcn_s_sleep(64);
         }
@@ -1609,6 +1627,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     int *wtop = s_wtop + wave;
     if (lane_id == 0) *wtop = 0;
     if (lane_id < 4) s_cnt[wave][lane_id] = 0;
+    if (threadIdx.x == 0 && C.early_q) __hip_atomic_store(C.bulk_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     Cold *cold = C.cold + gtid;
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
@@ -1830,7 +1849,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
          * a step (one lane-loop trip is ~7 us per step for it, the pair ~1.8 us) */
         if (C.early_q && !warm) {
             const bool early = active && L.phase == 0 && L.n_step >= C.early_steps;
-            if (__ballot(early) && __hip_atomic_load(C.early_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && early) {
+            if (__ballot(early) && __hip_atomic_load(C.early_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT) == 1 &&
+                early) {
                 const unsigned long long slot = atomicAdd(C.early_tail, 1ull);
                 if (slot < C.early_cap) {
                     export_lone(C.early_q + slot, L, cold);
@@ -2037,6 +2057,7 @@ struct grm_engine {
     int lone = 1;                          /* GRM_OPT_LONE */
     /* early hand-over of long photons to early_kernel on a second stream (GRM_OPT_EARLY_STEPS) */
     int early_steps = 5000;
+    bool early_serial = false; /* test: the worker ahead of the main launch on its stream */
     static constexpr unsigned long long EARLY_CAP = 1024;
     LoneRec *d_early = nullptr;
     unsigned long long *d_early_ready = nullptr;
@@ -2245,9 +2266,9 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
                                                                     C.admit_b0, std::min(h, C.admit_lim - h)));
         }
         /* the main launch runs the early worker beside it: [8] early tail, [9] head, [10] done,
-         * [11] workgroups exited, [12] worker running */
+         * [11] workgroups exited, [12] worker running / closed, [13] bulk started */
         const bool early = pass == 0 && C.pool_kind == 0 && e->early_steps > 0 && !C.lone_all && grid > 1;
-        if (early) op.set |= 0x1f00u;
+        if (early) op.set |= 0x3f00u;
         if (ctl(e, op, false)) return -1;
         if (early) {
             C.early_q = e->d_early;
@@ -2259,6 +2280,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.early_done = e->d_small + 10;
             C.wg_exit = e->d_small + 11;
             C.early_live = e->d_small + 12;
+            C.bulk_live = e->d_small + 13;
             C.early_steps = e->early_steps;
         } else {
             C.early_q = nullptr;
@@ -2277,7 +2299,11 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.pool_sh = 0;
             C.admit_n = 0;
         }
-        if (early) { /* after the control words are set; one workgroup, all of its pairs */
+        if (early && e->early_serial) { /* test: serialised ahead of the main launch */
+            hipLaunchKernelGGL(early_kernel, dim3(1), dim3(64 * 2 * LONE_PAIRS), 0, e->stream, e->P, C);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->ev_w, e->stream));
+        } else if (early) { /* after the control words are set; one workgroup, all of its pairs */
             HIPCHK(e, hipEventRecord(e->ev_pre, e->stream));
             HIPCHK(e, hipStreamWaitEvent(e->stream2, e->ev_pre, 0));
             hipLaunchKernelGGL(early_kernel, dim3(1), dim3(64 * 2 * LONE_PAIRS), 0, e->stream2, e->P, C);
@@ -2573,6 +2599,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
+    case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }

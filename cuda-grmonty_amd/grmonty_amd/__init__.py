@@ -51,6 +51,7 @@ OPT_WARMUP_SLACK = 12
 OPT_LONE = 13
 OPT_WARMUP_BATCH = 14
 OPT_EARLY_STEPS = 15
+OPT_EARLY_SERIAL = 16
 N_TH_BINS, N_E_BINS = 6, 200
 
 

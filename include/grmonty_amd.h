@@ -162,9 +162,12 @@ enum {
     /* photons of the first warm-up admission batch (default 64; later batches double the history) */
     GRM_OPT_WARMUP_BATCH = 14,
     /* a photon of this many steps (default 5000; 0 = off) leaves the lane loop at the top of a step
-     * for a two-wave pair of the early worker, which runs beside the main transport launch on the CU
-     * that launch leaves free */
-    GRM_OPT_EARLY_STEPS = 15
+     * for a two-wave pair of the early worker, which runs beside the main transport launch on a
+     * second stream */
+    GRM_OPT_EARLY_STEPS = 15,
+    /* test only: 1 launches the early worker on the transport stream ahead of the main launch, as a
+     * kernel-serialising tool (a counter profiler) would run them; the worker must then leave */
+    GRM_OPT_EARLY_SERIAL = 16
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

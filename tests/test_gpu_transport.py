@@ -38,14 +38,17 @@ def setup(model64, oracle64):
     return G, O, sel, snap, eng
 
 
-@pytest.mark.parametrize("lone", [1, 2, 3], ids=["lane-loop", "lone-kernel", "early-worker"])
+@pytest.mark.parametrize("lone", [1, 2, 3, 4], ids=["lane-loop", "lone-kernel", "early-worker", "early-serialised"])
 def test_photon_by_photon(setup, oracle64, lone):
     """lone=2 hands every photon to the lone-photon kernel (a two-wave pair per photon, halving walks
     over the lanes) at the top of its first step; lone=3 hands every photon that reaches 40 steps to
-    the concurrent early worker (up to its queue's 1024): those paths against the oracle"""
+    the concurrent early worker (up to its queue's 1024); lone=4 runs that worker ahead of the main
+    launch on its stream, as a kernel-serialising profiler would, so it must leave and take none:
+    those paths against the oracle"""
     G, O, sel, snap, eng = setup
-    eng.set_option(G.OPT_LONE, 1 if lone == 3 else lone)
-    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone == 3 else 5000)
+    eng.set_option(G.OPT_LONE, 1 if lone >= 3 else lone)
+    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone >= 3 else 5000)
+    eng.set_option(G.OPT_EARLY_SERIAL, 1 if lone == 4 else 0)
     oracle64.reset()
     tr_o = oracle64.track(sel, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=snap["scatt"],
                           rec0=snap["rec"], max_tau0=snap["maxtau"], trace_cap=4_000_000)
@@ -66,10 +69,13 @@ def test_photon_by_photon(setup, oracle64, lone):
     eng.set_option(G.OPT_BIAS_MODE, 0)
     eng.set_option(G.OPT_LONE, 1)
     eng.set_option(G.OPT_EARLY_STEPS, 5000)
+    eng.set_option(G.OPT_EARLY_SERIAL, 0)
     if lone == 2:
         assert st["n_lone"] >= len(sel) // 2, st["n_lone"]
     if lone == 3:
         assert st["n_early"] >= 200, st["n_early"]
+    if lone == 4:
+        assert st["n_early"] == 0, st["n_early"]
     assert st["n_dropped"] == 0
     assert st["n_primaries"] == len(sel)
     from parity_util import MIN_MATCH, check_spectrum_cells, trace_match
