@@ -604,6 +604,8 @@ __device__ __forceinline__ void load_ph2(const Slot &ph2, Lane &L) {
 __device__ bool init_photon(const Ctl &C, const Cold *cold, Lane &L, const Slot &ph2) {
     if (isnan(L.x[0]) || isnan(L.x[1]) || isnan(L.x[2]) || isnan(L.x[3]) || isnan(L.k[0]) || isnan(L.k[1]) ||
         isnan(L.k[2]) || isnan(L.k[3]) || L.w == 0.0) {
+        L.n_step = 0; /* the trace record is this photon's, not the lane's last one */
+        L.tau_abs() = L.tau_scatt() = 0.0;
         trace_end(C, cold, L, 4);
         return false;
     }
@@ -796,7 +798,7 @@ struct LonePair {
     LoneSlot ring[LONE_RING];
     LoneCtl ctl;
 };
-constexpr int LONE_PAIRS = 4; /* pairs of the concurrent worker (early_kernel, 8 waves) */
+constexpr int LONE_PAIRS = 2; /* pairs of the concurrent worker (early_kernel: 4 waves, one per SIMD, up to 512 VGPRs) */
 /* early_kernel waits this long (s_memrealtime, 100 MHz) for the bulk launch to start before it
  * takes the launches for serialised and leaves */
 constexpr unsigned long long EARLY_ALONE_TICKS = 100000; /* 1 ms */
