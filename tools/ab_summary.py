@@ -1,4 +1,4 @@
-"""Summarise tools/ab_libs.sh output: per variant, the single-pass transport rate (G steps/s) of
+"""Summarise tools/sessions/ab_libs.sh output: per variant, the single-pass transport rate (G steps/s) of
 every rep after the first (rep 0 carries the live-bias warm-up)."""
 import re
 import sys
