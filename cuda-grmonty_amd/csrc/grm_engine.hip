@@ -2300,6 +2300,10 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.pool_m = n_pool;
             C.pool_sh = 0;
             C.admit_n = 0;
+            /* a small relaunch (the children of the hand-overs, a few hundred) is a tail from its
+             * start: every photon goes to a two-wave pair at the top of its first step (~1.5 us per
+             * step against ~4 us in a sparse lane loop) */
+            C.lone_all = e->lone == 2 || (e->lone == 1 && n_pool <= e->lone_cap / 2);
         }
         if (early && e->early_serial) { /* test: serialised ahead of the main launch */
             hipLaunchKernelGGL(early_kernel, dim3(1), dim3(64 * 2 * LONE_PAIRS), 0, e->stream, e->P, C);
