@@ -832,15 +832,13 @@ __device__ __forceinline__ void unpack13(const double *d, double x[4], double k[
  * v_readlane -- a VALU instruction (plus hazard nops) per use, inside the step.  Passing the argument
  * block through an opaque SGPR copy at the top of each trip makes every use a scalar load from the
  * kernarg segment instead (constant address space: s_load, scalar cache, no VALU issue). */
-#ifndef GRM_KARG_LAUNDER
-#define GRM_KARG_LAUNDER 15
-#endif
 /* The kernarg segment of track_kernel / lone_kernel / early_kernel, all (Params, Ctl): explicit
  * arguments in order at their ABI alignment, i.e. the layout of this struct.  Two traps: the address
  * of a by-value kernel parameter is NOT the kernarg segment (taking it makes the compiler copy the
  * parameter into private memory), and __builtin_amdgcn_kernarg_segment_ptr() is only meaningful in
- * the kernel itself (in a called function it lowers to null).  So the kernel takes the pointer
- * (kargs()) and hands it down to non-inlined functions explicitly. */
+ * the kernel itself (in a called function it lowers to null): only the kernel takes the pointer
+ * (kargs()).  Used by track_kernel only: in the lone pipeline's serial chain the exposed scalar-load
+ * latency costs more than the readlanes (lone probe 1.80 vs 1.63 us/step, profiles/r02q_karg_ab.txt). */
 struct KArgs {
     Params P;
     Ctl C;
@@ -849,25 +847,22 @@ static_assert(offsetof(KArgs, C) == sizeof(Params), "kernarg layout: Ctl follows
 typedef const KArgs __attribute__((address_space(4))) KArgsK;
 /* call only in the body of a kernel whose explicit arguments are exactly (Params, Ctl) */
 __device__ __forceinline__ KArgsK *kargs() { return (KArgsK *)__builtin_amdgcn_kernarg_segment_ptr(); }
-template <class T, bool FRESH> __device__ __forceinline__ const T &karg(const T &v, KArgsK *ka) {
-    if constexpr (!FRESH) {
-        return v;
-    } else {
-        /* (a non-inlined function receives ka in VGPRs: make it scalar first; a no-op in a kernel) */
-        const uint64_t a = (uint64_t)ka;
-        KArgsK *k = (KArgsK *)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
-                               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
-        asm volatile("" : "+s"(k));
-        if constexpr (std::is_same<T, Params>::value)
-            return *(const Params *)&k->P;
-        else
-            return *(const Ctl *)&k->C;
-    }
+/* the kernarg segment through an opaque scalar copy of its pointer: loads through it cannot be
+ * hoisted out of the loop the copy is made in */
+__device__ __forceinline__ KArgsK *karg_fresh(KArgsK *ka) {
+    /* (a non-inlined function receives ka in VGPRs: make it scalar first; a no-op in a kernel) */
+    const uint64_t a = (uint64_t)ka;
+    KArgsK *k = (KArgsK *)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
+    asm volatile("" : "+s"(k));
+    return k;
 }
+__device__ __forceinline__ const Params &karg_params(KArgsK *k) { return *(const Params *)&k->P; }
+__device__ __forceinline__ const Ctl &karg_ctl(KArgsK *k) { return *(const Ctl *)&k->C; }
 
 /* The geometry wave of a pair (see above): runs photon after photon -- each begins as a restart
  * request from the interaction wave -- until LONE_STOP. */
-__device__ void lone_geometry(const Params &P_, const Ctl &C, KArgsK *ka, int lane, LonePair &pr) {
+__device__ void lone_geometry(const Params &P, const Ctl &C, int lane, LonePair &pr) {
     unsigned gen = 0;
     unsigned long long p = 0, cur = 0, cons = 0; /* cons: the last value read of pr.ctl.cons */
     bool spec = false; /* speculate the halving depths on this step's push (the last one halved) */
@@ -889,7 +884,6 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, KArgsK *ka, int la
     unsigned long long tg[6] = {0, 0, 0, 0, 0, 0}; /* steps, rounds, walk, step size, rest, halved */
 #endif
     while (true) {
-        const Params &P = karg<Params, (GRM_KARG_LAUNDER & 4) != 0>(P_, ka);
         if (p + 1 >= cons + LONE_RING) { /* the slot of step p and that of p - 1 must be consumed */
             cons = __hip_atomic_load(&pr.ctl.cons, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (p + 1 >= cons + LONE_RING) {
@@ -1036,9 +1030,7 @@ __device__ __forceinline__ bool lone_stop(const Params &P, double x1, double &w,
 
 /* The interaction wave of a pair: one handed-over photon, from its record to its end (the
  * geometry wave is started on it with a restart request: generation gen + 1, step 0). */
-__device__ void lone_interact(const Params &P_, const Ctl &C, KArgsK *ka, const LoneRec &R, int lane, LonePair &pr,
-                              unsigned &gen_io) {
-    const Params &P0 = P_;
+__device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, int lane, LonePair &pr, unsigned &gen_io) {
     double x1 = R.x[1];
     unsigned gen = gen_io + 1;
     if (lane == 0) {
@@ -1068,7 +1060,7 @@ __device__ void lone_interact(const Params &P_, const Ctl &C, KArgsK *ka, const 
     rng.ctr_hi = 0;
     double win = 0.0;
     uint32_t wbase = rng.ctr - 64u; /* empty window */
-    double bias_d = bias_den(P0, C);
+    double bias_d = bias_den(P, C);
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long steps = 0, children = 0;
     bool ended = false, abandoned = false;
@@ -1083,7 +1075,6 @@ __device__ void lone_interact(const Params &P_, const Ctl &C, KArgsK *ka, const 
     unsigned long long ti[4] = {0, 0, 0, 0}; /* batches, steps in them, batch-evaluation cycles, serial cycles */
 #endif
     while (!done) {
-        const Params &P = karg<Params, (GRM_KARG_LAUNDER & 8) != 0>(P_, ka);
         /* A batch: the consecutive steps the geometry wave has ready (at least one, at most
          * LONE_BATCH).  Lane j evaluates step si + j at once: the fluid and the absorption /
          * scattering coefficients at its end point (these depend on the geodesic only), and from
@@ -1345,8 +1336,8 @@ __device__ void lone_interact(const Params &P_, const Ctl &C, KArgsK *ka, const 
             atomicAdd(&C.ctr->n_abandoned, 1ull);
         } else if (ended) {
             /* record_criterion (:1066) when the stop criterion ended it, else the reason's trace */
-            if (reason < 0 && x[1] > P0.x1_max && n_step <= MAX_N_STEP)
-                record_photon(P0, C, cold, rng.id, w, x[1], x[2], x[3], tau_abs, tau_scatt, n_scatt, n_step,
+            if (reason < 0 && x[1] > P.x1_max && n_step <= MAX_N_STEP)
+                record_photon(P, C, cold, rng.id, w, x[1], x[2], x[3], tau_abs, tau_scatt, n_scatt, n_step,
                               reinterpret_cast<double *>(C.spec), (int)(sizeof(grm_spectrum_cell) / sizeof(double)));
             else if (C.trace)
                 write_trace(C, cold, rng.id, w, x[1], x[2], x[3], tau_abs, tau_scatt, n_scatt, n_step,
@@ -1375,11 +1366,11 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
     }
     __syncthreads();
     if (wave == 1) {
-        lone_geometry(P, C, kargs(), lane, pr);
+        lone_geometry(P, C, lane, pr);
         return;
     }
     unsigned gen = 0;
-    lone_interact(P, C, kargs(), C.lone[blockIdx.x], lane, pr, gen);
+    lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen);
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -1404,7 +1395,7 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
     if (wave & 1) {
-        lone_geometry(P, C, kargs(), lane, pr);
+        lone_geometry(P, C, lane, pr);
         return;
     }
     unsigned gen = 0;
@@ -1440,7 +1431,7 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
             __builtin_amdgcn_s_sleep(64);
         }
         if (!got) break;
-        lone_interact(P, C, kargs(), C.early_q[slot], lane, pr, gen);
+        lone_interact(P, C, C.early_q[slot], lane, pr, gen);
     }
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1703,8 +1694,9 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
 
     while (true) {
-        const Params &P = karg<Params, (GRM_KARG_LAUNDER & 1) != 0>(P_, ka);
-        const Ctl &C = karg<Ctl, (GRM_KARG_LAUNDER & 2) != 0>(C_, ka);
+        KArgsK *const kt = karg_fresh(ka); /* one opaque pointer for both (two would both spill) */
+        const Params &P = karg_params(kt);
+        const Ctl &C = karg_ctl(kt);
         ++wave_trips;
         TCOUNT(4);
         if (warm && blockIdx.x >= WARM_BLOCKS) {
