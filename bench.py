@@ -205,6 +205,10 @@ def main():
         id_base[sd] = sum(model.count(seed=sd, z0=a, z1=b, threads=threads) for a, b in shards[:rank])
     t_count = time.time() - t
     engine = G.Engine(model, device=local)
+    # A/B hook: GRM_BENCH_OPTS="15=2000,9=2" sets engine options (grmonty_amd.OPT_*) before the passes
+    for kv in filter(None, os.environ.get("GRM_BENCH_OPTS", "").split(",")):
+        k, v = kv.split("=")
+        engine.set_option(int(k), int(v))
     if world > 1:  # one RCCL communicator per rank
         uid = [G.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
