@@ -61,6 +61,57 @@ __device__ __forceinline__ double fratio_tol(double a, double b) {
     r = fma(r, fma(-b, r, 1.0), r);
     return fabs(a * r);
 }
+/* ---- polynomial coefficients from SGPRs ----
+ * d = a b + c for a compile-time constant c.  Left to itself the compiler evaluates a Horner step
+ * as v_fmac (d = c tied to the destination) and so first copies c into a VGPR pair: two v_mov_b32
+ * per coefficient per evaluation inside the persistent loop (machine LICM is off, see the Makefile),
+ * i.e. three VALU instructions per step of every polynomial.  With c as an SGPR operand of
+ * v_fma_f64 the copy is two s_mov_b32 on the scalar unit: one VALU instruction.  Same operation,
+ * same rounding. */
+__device__ __forceinline__ double fma_k(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+#define GRM_K(h) __builtin_bit_cast(double, (unsigned long long)(h))
+
+/* ocml's exp and exp10 (the same operations in the same order, so bit-identical results,
+ * tests/test_gpu_probes.py) with their coefficients through fma_k: k = rint(x log2 e), a two-part
+ * ln 2 reduction, a degree-11 minimax polynomial, ldexp; x > 1024 gives inf, x < -1075 zero. */
+__device__ __forceinline__ double exp_poly(double r) {
+    double p = fma_k(r, GRM_K(0x3e5ade156a5dcb37ull), GRM_K(0x3e928af3fca7ab0cull));
+    p = fma_k(r, p, GRM_K(0x3ec71dee623fde64ull));
+    p = fma_k(r, p, GRM_K(0x3efa01997c89e6b0ull));
+    p = fma_k(r, p, GRM_K(0x3f2a01a014761f6eull));
+    p = fma_k(r, p, GRM_K(0x3f56c16c1852b7b0ull));
+    p = fma_k(r, p, GRM_K(0x3f81111111122322ull));
+    p = fma_k(r, p, GRM_K(0x3fa55555555502a1ull));
+    p = fma_k(r, p, GRM_K(0x3fc5555555555511ull));
+    p = fma_k(r, p, GRM_K(0x3fe000000000000bull));
+    p = fma(r, p, 1.0);
+    return fma(r, p, 1.0);
+}
+__device__ __forceinline__ double exp_range(double x, double y) {
+    y = x > 1024.0 ? __builtin_huge_val() : y;
+    return x < -1075.0 ? 0.0 : y;
+}
+__device__ __forceinline__ double fexp(double x) {
+    const double k = __builtin_rint(x * GRM_K(0x3ff71547652b82feull));
+    double r = fma(GRM_K(0xbfe62e42fefa39efull), k, x);
+    r = fma(GRM_K(0xbc7abc9e3b39803full), k, r);
+    const double p = exp_poly(r);
+    return exp_range(x, __builtin_amdgcn_ldexp(p, (int)k));
+}
+__device__ __forceinline__ double fexp10(double x) {
+    const double k = __builtin_rint(x * GRM_K(0x400a934f0979a371ull));
+    double r = fma(GRM_K(0xbfd34413509f79ffull), k, x);
+    r = fma(GRM_K(0x3c49dc1da994fd21ull), k, r);
+    double z = r * GRM_K(0xbcaf48ad494ea3e9ull);
+    z = fma(GRM_K(0x40026bb1bbb55516ull), r, z);
+    const double p = exp_poly(z);
+    return exp_range(x, __builtin_amdgcn_ldexp(p, (int)k));
+}
+
 /* ---- natural logarithm ----
  * ocml's log carries a double-double evaluation for < 0.5-ulp results (~90 VALU ops).  flog is the
  * classic fdlibm reduction (x = 2^e m, m in [sqrt(1/2), sqrt(2)), s = (m-1)/(m+1), log m =
@@ -78,9 +129,12 @@ __device__ __forceinline__ double flog(double x) {
     const double f = m - 1.0;
     const double s = fdiv(f, 2.0 + f);
     const double z = s * s, w = z * z;
-    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
-    const double t2 = z * (6.666666666666735130e-01 +
-                           w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    const double t1 =
+        w * fma_k(w, fma_k(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 = z * fma_k(w,
+                                fma_k(w, fma_k(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                                      2.857142874366239149e-01),
+                                6.666666666666735130e-01);
     const double r = t2 + t1;
     const double hfsq = 0.5 * f * f;
     const double dk = (double)e;
@@ -96,22 +150,22 @@ __device__ __forceinline__ void fsincospi(double x, double &s, double &c) {
     const double r = fma(n, -0.5, x);
     const double t = r * r;
     double ps = 7.952054001475513e-07;
-    ps = fma(ps, t, -2.1915353447830217e-05);
-    ps = fma(ps, t, 0.00046630280576761255);
-    ps = fma(ps, t, -0.0073704309457143504);
-    ps = fma(ps, t, 0.08214588661112823);
-    ps = fma(ps, t, -0.5992645293207921);
-    ps = fma(ps, t, 2.5501640398773455);
-    ps = fma(ps, t, -5.16771278004997);
+    ps = fma_k(ps, t, -2.1915353447830217e-05);
+    ps = fma_k(ps, t, 0.00046630280576761255);
+    ps = fma_k(ps, t, -0.0073704309457143504);
+    ps = fma_k(ps, t, 0.08214588661112823);
+    ps = fma_k(ps, t, -0.5992645293207921);
+    ps = fma_k(ps, t, 2.5501640398773455);
+    ps = fma_k(ps, t, -5.16771278004997);
     const double sr = fma(r * t, ps, r * 3.141592653589793); /* r (pi + t P(t)) */
     double pc = 4.303069587032947e-06;
-    pc = fma(pc, t, -0.0001046381049248457);
-    pc = fma(pc, t, 0.0019295743094039231);
-    pc = fma(pc, t, -0.02580689139001406);
-    pc = fma(pc, t, 0.2353306303588932);
-    pc = fma(pc, t, -1.3352627688545895);
-    pc = fma(pc, t, 4.0587121264167685);
-    pc = fma(pc, t, -4.934802200544679);
+    pc = fma_k(pc, t, -0.0001046381049248457);
+    pc = fma_k(pc, t, 0.0019295743094039231);
+    pc = fma_k(pc, t, -0.02580689139001406);
+    pc = fma_k(pc, t, 0.2353306303588932);
+    pc = fma_k(pc, t, -1.3352627688545895);
+    pc = fma_k(pc, t, 4.0587121264167685);
+    pc = fma_k(pc, t, -4.934802200544679);
     const double cr = fma(t, pc, 1.0);
     const int q = (int)n;
     const bool odd = (q & 1) != 0;
@@ -224,7 +278,7 @@ struct Trig {
  * sincospi of x2-scaled arguments -- an exact, branch-free range reduction instead of the general
  * one (agreement with sin/cos of the pi-multiplied argument to a few ulp) */
 __device__ __forceinline__ void trig_at(const Params &P, const double x[4], Trig &T) {
-    T.r1 = exp(x[1]);
+    T.r1 = fexp(x[1]);
     fsincospi(2.0 * x[2], T.s2x, T.c2x);
     fsincospi(x[2] + ((1.0 - P.h_slope) / (2.0 * kPi)) * T.s2x, T.sth, T.cth);
 }
@@ -792,7 +846,7 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
     if (xb < 1.0e-3)
         b_nu = fdiv(2.0 * HPL / (CL * CL), xb * (1.0 / 24.0) * (24.0 + xb * (12.0 + xb * (4.0 + xb))));
     else
-        b_nu = fdiv(2.0 * HPL / (CL * CL), exp(xb) - 1.0);
+        b_nu = fdiv(2.0 * HPL / (CL * CL), fexp(xb) - 1.0);
     /* scattering: kappa_es * nu * n_e * m_p */
     double sigma;
     if (hc_thomson) {
@@ -805,7 +859,7 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
         const double d_i = fi - i, d_j = fj - j;
         const double lc =
             (1.0 - d_i) * (1.0 - d_j) * t00 + d_i * (1.0 - d_j) * t10 + (1.0 - d_i) * d_j * t01 + d_i * d_j * t11;
-        sigma = exp10(lc);
+        sigma = fexp10(lc);
     }
     a_s = nu * sigma * n_e; /* nu kappa n_e m_p, kappa = sigma / m_p */
     /* absorption: j_nu / nu^2 / (B_nu / nu^3) */
@@ -820,7 +874,7 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
             dk -= ik;
             l_k2 = (1.0 - dk) * k2a + dk * k2b;
         }
-        jnu = ((kSqrt2 * kPi * EE * EE / (3.0 * CL)) * n_e * nu_s) * f * exp(-xp - l_k2);
+        jnu = ((kSqrt2 * kPi * EE * EE / (3.0 * CL)) * n_e * nu_s) * f * fexp(-xp - l_k2);
     }
     a_a = fdiv(jnu, nu * nu * (b_nu + 1.0e-100));
 }

@@ -1158,7 +1158,7 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
             }
             const double d_tau = l_dta + l_dts;
             l_fac = d_tau < 1.0e-3 ? (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))))
-                                   : exp(-d_tau);
+                                   : fexp(-d_tau);
         }
 #ifdef GRM_TIMING
         const unsigned long long tb1 = __builtin_amdgcn_s_memtime();
@@ -1225,7 +1225,7 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
                     if (d_tau_abs < 1.0e-3)
                         w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
                     else
-                        w *= exp(-d_tau);
+                        w *= fexp(-d_tau);
                     /* photon_2 pushed to the scattering point (:1005-1010), by this wave */
                     double x[4], k[4], dk[4], e_0_s;
                     /* photon_2 of this step: the state after the step before, or the restart state */
@@ -1593,7 +1593,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
                 if (d_tau_abs < 1.0e-3)
                     L.w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
                 else
-                    L.w *= exp(-d_tau);
+                    L.w *= fexp(-d_tau);
                 /* re-push photon_2 by dl*frac to the scattering point (:1005), on later trips */
                 load_ph2(ph2, L);
                 L.e_0_s = L.ph2_e0s();
@@ -1614,7 +1614,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             if (d_tau < 1.0e-3)
                 L.w *= (1.0 - d_tau * (1.0 / 24.0) * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
             else
-                L.w *= exp(-d_tau);
+                L.w *= fexp(-d_tau);
             L.tau_abs() += d_tau_abs;
             L.tau_scatt() += d_tau_scatt;
         }

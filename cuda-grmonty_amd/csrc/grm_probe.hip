@@ -25,6 +25,8 @@
  * 18     seed id dof                                chi^2 sample, ctr
  * 19     x                                          flog(x), ocml log(x)
  * 20     x                                          fsincospi(x) s c, ocml sincospi(x) s c
+ * 21     x                                          fexp(x), ocml exp(x)
+ * 22     x                                          fexp10(x), ocml exp10(x)
  */
 #include <hip/hip_runtime.h>
 
@@ -220,6 +222,14 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
         store(o, 3, c1);
         break;
     }
+    case 21:
+        store(o, 0, fexp(a[0]));
+        store(o, 1, exp(a[0]));
+        break;
+    case 22:
+        store(o, 0, fexp10(a[0]));
+        store(o, 1, exp10(a[0]));
+        break;
     default: break;
     }
 }
@@ -229,7 +239,7 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
 extern "C" int grm_probe_impl(const Params &P, hipStream_t s, int which, const double *in, int in_stride, double *out,
                               int out_stride, size_t n, std::string &err) {
     if (n == 0) return 0;
-    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 20) {
+    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 22) {
         err = "grm_probe: bad arguments";
         return -1;
     }

@@ -316,3 +316,17 @@ def test_fsincospi_accuracy(engine):
           f"sin {err(dev[:, 2], ref_s).max():.2f} cos {err(dev[:, 3], ref_c).max():.2f}")
     assert es.max() <= 2.0 and ec.max() <= 2.0
     assert np.signbit(dev[-2, 0]) and dev[-1, 0] == np.pi * 1e-300 or abs(dev[-1, 0] - np.pi * 1e-300) < 1e-315
+
+
+def test_fexp_bitwise_ocml(engine):
+    """fexp / fexp10 (grm_device.h: ocml's exp / exp10 with the polynomial coefficients in SGPRs)
+    are bit-identical to ocml's exp / exp10 over the whole range, overflow, underflow and specials
+    included."""
+    rng = np.random.default_rng(11)
+    x = np.concatenate([rng.uniform(-1100, 1100, 4000), rng.uniform(-750, 720, 4000), rng.uniform(-5, 5, 4000),
+                        rng.uniform(-1e-3, 1e-3, 500), np.arange(-30, 31) * np.log(2.0),
+                        [0.0, -0.0, 1.0, 709.78, 709.79, -745.1, -745.2, 1024.0, 1024.5, -1075.0, -1075.5,
+                         1e300, -1e300, np.inf, -np.inf, np.nan]])
+    for which in (21, 22):
+        d = engine.probe(which, x[:, None], 2)
+        np.testing.assert_array_equal(d[:, 0].view(np.uint64), d[:, 1].view(np.uint64))

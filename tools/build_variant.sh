@@ -7,7 +7,7 @@ name=$1
 D="$R/cuda-grmonty_amd/build/var_$name"; mkdir -p "$D" "$R/cuda-grmonty_amd/variants"
 make -s -C "$R/cuda-grmonty_amd" build/grm_host.o build/grm_probe.o build/grm_emit.o build/grm_tables.o
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -mllvm -disable-machine-licm"
-SCHED=${SCHED:-iterative-ilp}; SF=""; [ "$SCHED" = none ] || SF="-mllvm -amdgpu-sched-strategy=$SCHED"
+SCHED=${SCHED:-none}; SF=""; [ "$SCHED" = none ] || SF="-mllvm -amdgpu-sched-strategy=$SCHED"
 /opt/rocm/bin/hipcc $FL $SF $VFLAGS -c "$R/cuda-grmonty_amd/csrc/grm_engine.hip" -o "$D/grm_engine.o"
 B="$R/cuda-grmonty_amd/build"
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/cuda-grmonty_amd/variants/libgrmonty_amd_v$name.so" \

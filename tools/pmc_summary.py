@@ -31,8 +31,7 @@ if g("TCC_HIT_sum") is not None and g("TCC_REQ_sum"):
     print(f"L2 hit rate                 {g('TCC_HIT_sum') / max(1.0, g('TCC_HIT_sum') + g('TCC_MISS_sum')):.3f}")
 if steps:
     print(f"transport steps (pass)      {steps}")
-    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_INSTS_VALU_FMA_F64",
-              "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64"):
+    for k in sorted(k for k in tot if k.startswith("SQ_INSTS")):
         if g(k):
             print(f"{k + ' / step (wave instr)':44s} {g(k) / steps:.2f}")
     if g("FETCH_SIZE") is not None and g("WRITE_SIZE") is not None:
