@@ -215,35 +215,50 @@ def main():
         engine.comm_init(uid[0], world, rank)
     engine.emit_setup(model)  # the zone table is resident in HBM before the timed region
 
-    def one_pass(eng, seed, base, allreduce):
-        """one run_simulation pass: emission + transport + reduction + readback"""
+    def one_pass(eng, seed, base, slot):
+        """one run_simulation pass on this rank's shard: emission + transport + readback; with
+        several ranks its results are stashed on the device (slot) for the job's one all-reduce"""
         eng.reset()
         eng.set_option(G.OPT_SEED, seed)
         eng.set_option(G.OPT_ID_BASE, base)
         ptr, n_dev = eng.emit(seed=seed, z0=z0, z1=z1)
         eng.track_device(ptr, n_dev)
         st = eng.stats()
-        if allreduce:
-            eng.allreduce()
+        if slot is not None:
+            eng.stash(slot)
         spec, n_rec, n_scatt, max_tau = eng.finish()
         if st["n_dropped"] or st["n_abandoned"]:
             raise RuntimeError(f"pass seed {seed}: {st['n_dropped']} children dropped, {st['n_abandoned']} abandoned")
         return n_dev, st, n_rec, n_scatt
 
-    for sd in warm_seeds:
-        one_pass(engine, sd, id_base[sd], world > 1)
+    def reduce_job(eng, n):
+        """the job's one exchange: a grouped RCCL all-reduce of every pass's stashed results, then
+        each pass's reduced spectrum and counters read back (the ranks' pass timelines stay
+        uncoupled: a rank held up by a long-lived photon does not stall the others pass by pass)"""
+        eng.allreduce_stash(n)
+        return [eng.stash_read(s) for s in range(n)]
+
+    if world > 1:
+        engine.stash_reserve(max(len(warm_seeds), len(timed_seeds)))
+    for i, sd in enumerate(warm_seeds):
+        one_pass(engine, sd, id_base[sd], i if world > 1 else None)
+    if world > 1 and warm_seeds:
+        reduce_job(engine, len(warm_seeds))
     launches0 = engine.stats()["n_launches"]
     if dist is not None:
         dist.barrier()
     res, pass_s = [], []
     t0 = time.time()
-    for sd in timed_seeds:
+    for i, sd in enumerate(timed_seeds):
         tp = time.time()
-        res.append(one_pass(engine, sd, id_base[sd], world > 1))
+        res.append(one_pass(engine, sd, id_base[sd], i if world > 1 else None))
         pass_s.append(time.time() - tp)
+    job = reduce_job(engine, len(timed_seeds)) if world > 1 else None
     if dist is not None:
         dist.barrier()
     elapsed = time.time() - t0
+    if job is not None:  # the job-level results: the reduced counters of every pass
+        res = [(r[0], r[1], j[1], j[2]) for r, j in zip(res, job)]
     n_rank = sum(r[0] for r in res)
     tmax, total = elapsed, n_rank
     if dist is not None:
@@ -295,7 +310,8 @@ def main():
                                    f"mass_unit=4e19, zone-sharded over {world} GPU(s)",
                        "photon_n_job": photon_n_job, "grid": f"{args.grid}x{args.grid}",
                        "superphotons_per_pass_rank0": n_rank // max(1, args.steps),
-                       "parallelism": f"zone shards x{world}, RCCL spectrum all-reduce"},
+                       "parallelism": f"zone shards x{world}" + (", passes stashed on the device, one RCCL all-reduce per job"
+                                                                  if world > 1 else "")},
             "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": achieved_tf / FP64_PEAK_TFS if achieved_tf else None,
                          "traffic": traffic,

@@ -2028,6 +2028,31 @@ struct CtlOp {
     unsigned long long max_tau_init_bits;
 };
 
+/* one pass's results into slot `slot` of the stash (grm_engine_stash): the spectrum, then the
+ * counters split by their reduction (sum: recorded, scattered, steps, tracked, children, overflow,
+ * dropped, primaries, lives > 1e5; max: max tau_scatt bits, longest life) */
+constexpr int STASH_SUMS = 9, STASH_MAXS = 2;
+__global__ __launch_bounds__(256) void stash_kernel(const double *spec, const DevCounters *ctr, double *st_spec,
+                                                    unsigned long long *st_sum, unsigned long long *st_max, int slot,
+                                                    int ncell) {
+    double *dst = st_spec + (size_t)slot * ncell;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < ncell; i += gridDim.x * 256) dst[i] = spec[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        unsigned long long *s = st_sum + (size_t)slot * STASH_SUMS, *m = st_max + (size_t)slot * STASH_MAXS;
+        s[0] = ctr->n_recorded;
+        s[1] = ctr->n_scatt;
+        s[2] = ctr->n_steps;
+        s[3] = ctr->n_tracked;
+        s[4] = ctr->n_children;
+        s[5] = ctr->n_overflow;
+        s[6] = ctr->n_dropped;
+        s[7] = ctr->n_primaries;
+        s[8] = ctr->n_long;
+        m[0] = ctr->max_tau_bits;
+        m[1] = ctr->max_nstep;
+    }
+}
+
 __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
     if (op.reset)
         for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < op.n_spec; i += (size_t)gridDim.x * 256)
@@ -2091,6 +2116,11 @@ struct grm_engine {
     grm_init_photon *d_upload = nullptr;
     size_t upload_cap = 0;
     ncclComm_t comm = nullptr;
+    /* deferred reduction of a job's passes (grm_engine_stash*): per slot the spectrum, 9 summed
+     * counters and 2 max counters */
+    double *d_stash_spec = nullptr;
+    unsigned long long *d_stash_sum = nullptr, *d_stash_max = nullptr;
+    int stash_cap = 0;
     unsigned long long *d_timing = nullptr;
     unsigned long long *d_waves = nullptr; /* [lanes / 64][4] per-wave record of the last launch */
     int64_t watchdog_ms = 60000;           /* per-launch watchdog (GRM_OPT_WATCHDOG_MS; 0 = off) */
@@ -2605,6 +2635,9 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_eoff);
     hipFree(e->d_emit);
     if (e->comm) ncclCommDestroy(e->comm);
+    hipFree(e->d_stash_spec);
+    hipFree(e->d_stash_sum);
+    hipFree(e->d_stash_max);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
     if (e->ev2) hipEventDestroy(e->ev2);
@@ -2902,6 +2935,98 @@ int grm_engine_allreduce(grm_engine *e) {
         return -1;
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int grm_engine_stash_reserve(grm_engine *e, int n_slots) {
+    if (!e || n_slots < 0) return -1;
+    if (n_slots <= e->stash_cap) return 0;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const size_t ncell = (size_t)N_TH_BINS * N_E_BINS * (sizeof(grm_spectrum_cell) / sizeof(double));
+    hipFree(e->d_stash_spec);
+    hipFree(e->d_stash_sum);
+    hipFree(e->d_stash_max);
+    e->d_stash_spec = nullptr;
+    e->d_stash_sum = e->d_stash_max = nullptr;
+    e->stash_cap = 0;
+    HIPCHK(e, hipMalloc(&e->d_stash_spec, (size_t)n_slots * ncell * sizeof(double)));
+    HIPCHK(e, hipMalloc(&e->d_stash_sum, (size_t)n_slots * STASH_SUMS * sizeof(unsigned long long)));
+    HIPCHK(e, hipMalloc(&e->d_stash_max, (size_t)n_slots * STASH_MAXS * sizeof(unsigned long long)));
+    e->stash_cap = n_slots;
+    return 0;
+}
+
+int grm_engine_stash(grm_engine *e, int slot) {
+    if (!e) return -1;
+    if (slot < 0 || slot >= e->stash_cap) {
+        e->err = "grm_engine_stash: slot " + std::to_string(slot) + " outside the reserved " +
+                 std::to_string(e->stash_cap) + " (grm_engine_stash_reserve)";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    const int ncell = N_TH_BINS * N_E_BINS * (int)(sizeof(grm_spectrum_cell) / sizeof(double));
+    hipLaunchKernelGGL(stash_kernel, dim3(8), dim3(256), 0, e->stream, reinterpret_cast<const double *>(e->d_spec),
+                       e->d_ctr, e->d_stash_spec, e->d_stash_sum, e->d_stash_max, slot, ncell);
+    HIPCHK(e, hipGetLastError());
+    return 0;
+}
+
+int grm_engine_allreduce_stash(grm_engine *e, int n_slots) {
+    if (!e) return -1;
+    if (n_slots < 0 || n_slots > e->stash_cap) {
+        e->err = "grm_engine_allreduce_stash: bad slot count";
+        return -1;
+    }
+    if (!e->comm) {
+        e->err = "grm_engine_allreduce_stash: no communicator (grm_engine_comm_init)";
+        return -1;
+    }
+    if (n_slots == 0) return 0;
+    HIPCHK(e, hipSetDevice(e->device));
+    const size_t ncell = (size_t)N_TH_BINS * N_E_BINS * (sizeof(grm_spectrum_cell) / sizeof(double));
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess)
+        r = ncclAllReduce(e->d_stash_spec, e->d_stash_spec, (size_t)n_slots * ncell, ncclFloat64, ncclSum, e->comm,
+                          e->stream);
+    if (r == ncclSuccess)
+        r = ncclAllReduce(e->d_stash_sum, e->d_stash_sum, (size_t)n_slots * STASH_SUMS, ncclUint64, ncclSum, e->comm,
+                          e->stream);
+    if (r == ncclSuccess)
+        r = ncclAllReduce(e->d_stash_max, e->d_stash_max, (size_t)n_slots * STASH_MAXS, ncclUint64, ncclMax, e->comm,
+                          e->stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess) {
+        e->err = std::string("RCCL all-reduce (stash): ") + ncclGetErrorString(r);
+        return -1;
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int grm_engine_stash_read(grm_engine *e, int slot, grm_spectrum_cell *spec, uint64_t *n_rec, uint64_t *n_scatt,
+                          double *max_tau, uint64_t *n_steps) {
+    if (!e) return -1;
+    if (slot < 0 || slot >= e->stash_cap) {
+        e->err = "grm_engine_stash_read: slot outside the reserved stash";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    const size_t ncell = (size_t)N_TH_BINS * N_E_BINS * (sizeof(grm_spectrum_cell) / sizeof(double));
+    unsigned long long sums[STASH_SUMS], maxs[STASH_MAXS];
+    if (spec)
+        HIPCHK(e, hipMemcpyAsync(spec, e->d_stash_spec + (size_t)slot * ncell, ncell * sizeof(double),
+                                 hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(sums, e->d_stash_sum + (size_t)slot * STASH_SUMS, sizeof(sums), hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipMemcpyAsync(maxs, e->d_stash_max + (size_t)slot * STASH_MAXS, sizeof(maxs), hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (n_rec) *n_rec = sums[0];
+    if (n_scatt) *n_scatt = sums[1];
+    if (n_steps) *n_steps = sums[2];
+    if (max_tau) std::memcpy(max_tau, &maxs[0], sizeof(double));
     return 0;
 }
 

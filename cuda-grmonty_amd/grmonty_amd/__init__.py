@@ -123,6 +123,11 @@ SIGNATURES = {
     "grm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "grm_engine_comm_init": (C.c_int, [VP, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     "grm_engine_allreduce": (C.c_int, [VP]),
+    "grm_engine_stash_reserve": (C.c_int, [VP, C.c_int]),
+    "grm_engine_stash": (C.c_int, [VP, C.c_int]),
+    "grm_engine_allreduce_stash": (C.c_int, [VP, C.c_int]),
+    "grm_engine_stash_read": (C.c_int, [VP, C.c_int, VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
     "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_stuck": (C.c_int64, [VP, VP, C.c_size_t]),
@@ -399,6 +404,24 @@ class Engine:
 
     def allreduce(self):
         self._check(self.L.grm_engine_allreduce(self.h))
+
+    # deferred reduction: stash each pass's results on the device, one all-reduce for the job
+    def stash_reserve(self, n_slots: int):
+        self._check(self.L.grm_engine_stash_reserve(self.h, int(n_slots)))
+
+    def stash(self, slot: int):
+        self._check(self.L.grm_engine_stash(self.h, int(slot)))
+
+    def allreduce_stash(self, n_slots: int):
+        self._check(self.L.grm_engine_allreduce_stash(self.h, int(n_slots)))
+
+    def stash_read(self, slot: int):
+        """(spectrum, n_recorded, n_scatt, max_tau_scatt, n_steps) of a stashed pass"""
+        spec = np.zeros(N_TH_BINS * N_E_BINS, dtype=SPECTRUM_CELL)
+        nr, ns, mt, st = C.c_uint64(), C.c_uint64(), C.c_double(), C.c_uint64()
+        self._check(self.L.grm_engine_stash_read(self.h, int(slot), _ptr(spec), C.byref(nr), C.byref(ns), C.byref(mt),
+                                                 C.byref(st)))
+        return spec.reshape(N_TH_BINS, N_E_BINS), nr.value, ns.value, mt.value, st.value
 
     def probe(self, which: int, inputs: np.ndarray, out_width: int) -> np.ndarray:
         a = np.ascontiguousarray(inputs, dtype=np.float64)

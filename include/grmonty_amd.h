@@ -225,6 +225,18 @@ int grm_engine_comm_init(grm_engine *e, const uint8_t id[128], int nranks, int r
 /* in-place all-reduce of the spectrum (fp64 sum), counters (u64 sum) and max tau_scatt (max):
  * the only exchange step of the path (photon shards are independent). */
 int grm_engine_allreduce(grm_engine *e);
+/* One end-of-job exchange instead of one per pass: a rank runs its passes (run_simulation calls)
+ * back to back, stashing each pass's results on the device (grm_engine_stash after the pass's
+ * transport, into one of grm_engine_stash_reserve's slots), then ONE grouped RCCL all-reduce of all
+ * slots (grm_engine_allreduce_stash: spectra and counters summed, max tau_scatt and longest life
+ * maxed) and reads each pass's reduced result (grm_engine_stash_read).  The ranks' pass timelines
+ * are then not coupled pass by pass (a rank with a long-lived photon in one pass does not hold the
+ * others at that pass).  Same reduction as grm_engine_allreduce (harm_model.cpp:340-414 is one pass). */
+int grm_engine_stash_reserve(grm_engine *e, int n_slots);
+int grm_engine_stash(grm_engine *e, int slot);
+int grm_engine_allreduce_stash(grm_engine *e, int n_slots);
+int grm_engine_stash_read(grm_engine *e, int slot, grm_spectrum_cell *spec, uint64_t *n_rec, uint64_t *n_scatt,
+                          double *max_tau, uint64_t *n_steps);
 
 /* --- host model (harm_model.hpp; C++ host, no GPU) ------------------------------------- */
 typedef struct grm_model grm_model;

@@ -91,3 +91,78 @@ def test_two_rank_shards_equal_single_job(dump32, tmp_path):
     ctr_1 = pack_counters(orc)
     np.testing.assert_array_equal(ctr_d, ctr_1)  # counts exact, max tau_scatt bit-exact
     np.testing.assert_allclose(spec_d, spec_1, rtol=1e-12, atol=0)
+
+
+STASH_SEEDS = (123, 124)
+
+
+def stash_counters(orc):
+    """one pass's counters as grm_engine_stash lays them out: 9 summed words (recorded, scattered,
+    steps, tracked, children, overflow, dropped, primaries, lives > 1e5) and 2 maxed (max tau_scatt
+    bits, longest life); the oracle fills the words it has"""
+    c = orc.counters()
+    s = np.zeros(9, dtype=np.int64)
+    s[0], s[1], s[2], s[7] = c["recorded"], c["scattered"], c["steps"], c["created"]
+    m = np.zeros(2, dtype=np.int64)
+    m[0] = np.array([orc.scalars()["max_tau_scatt"]], dtype=np.float64).view(np.int64)[0]
+    return s, m
+
+
+def _stash_job(rank, world, dump, out_dir, port):
+    """several passes per rank, each stashed, then ONE grouped reduction of all of them
+    (grm_engine_allreduce_stash: spectra SUM, 9 counters SUM, 2 counters MAX -- over gloo here)"""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "cuda-grmonty_amd"), os.path.join(os.path.dirname(here), "oracle")]
+    import grmonty_amd as G
+    import oracle_py as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    model = G.Model.load(dump, photon_n=150 * world).init(2)
+    shards = G.shard_zones(model.zone_weights(), world)
+    k = len(STASH_SEEDS)
+    st_spec = np.zeros((k, 15600))
+    st_sum = np.zeros((k, 9), dtype=np.int64)
+    st_max = np.zeros((k, 2), dtype=np.int64)
+    for slot, seed in enumerate(STASH_SEEDS):
+        counts = [model.count(seed=seed, z0=a, z1=b) for a, b in shards]
+        ph = model.emit(seed=seed, z0=shards[rank][0], z1=shards[rank][1])
+        orc = O.OracleModel(dump, photon_n=150 * world)
+        orc.init(2)
+        orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=seed, id_base=int(sum(counts[:rank])), frozen=True,
+                  scatt0=SNAP["scatt"], rec0=SNAP["rec"], max_tau0=SNAP["maxtau"])
+        st_spec[slot] = orc.spectrum().view(np.float64).reshape(-1)
+        st_sum[slot], st_max[slot] = stash_counters(orc)
+    spec, ssum, smax = torch.from_numpy(st_spec), torch.from_numpy(st_sum), torch.from_numpy(st_max)
+    dist.all_reduce(spec, op=dist.ReduceOp.SUM)
+    dist.all_reduce(ssum, op=dist.ReduceOp.SUM)
+    dist.all_reduce(smax, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "st_spec.npy"), spec.numpy())
+        np.save(os.path.join(out_dir, "st_sum.npy"), ssum.numpy())
+        np.save(os.path.join(out_dir, "st_max.npy"), smax.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_stashed_passes_equal_single_jobs(dump32, tmp_path):
+    """bench.py's multi-GPU exchange: every pass stashed, one reduction for the job; each reduced slot
+    must equal one process running that pass's whole job"""
+    import grmonty_amd as G
+    import oracle_py as O
+    world = 2
+    mp.spawn(_stash_job, args=(world, dump32, str(tmp_path), _free_port()), nprocs=world, join=True)
+    st_spec = np.load(tmp_path / "st_spec.npy")
+    st_sum = np.load(tmp_path / "st_sum.npy")
+    st_max = np.load(tmp_path / "st_max.npy")
+    model = G.Model.load(dump32, photon_n=150 * world).init(2)
+    for slot, seed in enumerate(STASH_SEEDS):
+        ph = model.emit(seed=seed)
+        orc = O.OracleModel(dump32, photon_n=150 * world)
+        orc.init(2)
+        orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=seed, id_base=0, frozen=True, scatt0=SNAP["scatt"],
+                  rec0=SNAP["rec"], max_tau0=SNAP["maxtau"])
+        s1, m1 = stash_counters(orc)
+        np.testing.assert_array_equal(st_sum[slot], s1)
+        np.testing.assert_array_equal(st_max[slot], m1)
+        np.testing.assert_allclose(st_spec[slot], orc.spectrum().view(np.float64).reshape(-1), rtol=1e-12, atol=0)
