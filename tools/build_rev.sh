@@ -14,7 +14,8 @@ git -C "$R" show "$rev:include/grmonty_amd.h" > "$D/include/grmonty_amd.h"
 sed -i 's|"../../include/grmonty_amd.h"|"../include/grmonty_amd.h"|' "$D/csrc/"*.h "$D/csrc/"*.hip
 make -s -C "$R/cuda-grmonty_amd" build/grm_host.o
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -mllvm -disable-machine-licm"
-/opt/rocm/bin/hipcc $FL -mllvm -amdgpu-sched-strategy=iterative-ilp $VFLAGS -c "$D/csrc/grm_engine.hip" -o "$D/grm_engine.o" &
+SF=""; [ -n "$SCHED" ] && SF="-mllvm -amdgpu-sched-strategy=$SCHED"  # revisions before 58fc566 were built with SCHED=iterative-ilp
+/opt/rocm/bin/hipcc $FL $SF $VFLAGS -c "$D/csrc/grm_engine.hip" -o "$D/grm_engine.o" &
 objs="$D/grm_engine.o"
 for f in grm_probe grm_emit grm_tables; do
   [ -f "$D/csrc/$f.hip" ] || continue
