@@ -128,7 +128,12 @@ def cpu_baseline(path: str, photon_n: int, photons: np.ndarray, seconds: float):
             "sample": f"{done} of the {len(photons)} superphotons of pass 0 (random subset) tracked in {t_track:.1f} s "
                       f"+ {n_em} superphotons emitted from random zones in {t_emit:.1f} s by the oracle "
                       f"(oracle/grmonty_oracle.cpp: serial reference CPU semantics, mt19937, live bias) on 1 "
-                      f"host core; the reference's own CPU build is not buildable here (DESIGN.md §3)"}
+                      f"host core; the reference's own CPU build is not buildable here (DESIGN.md §3)",
+            "ratio_R": None,
+            "ratio_R_note": "R = reference CPU build rate / this oracle's rate on the same dump is not measurable here: "
+                            "the reference CPU build needs spdlog/<format> stand-ins, which this pipeline does not allow; "
+                            "the survey measured that build at ~3.2 k superphotons/s on its own synthetic 192^2 dump "
+                            "(BASELINE.md section 2, a dump scattering ~3x more per photon than this one)"}
 
 
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
