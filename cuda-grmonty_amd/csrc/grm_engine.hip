@@ -76,7 +76,8 @@ struct DevCounters {
     unsigned long long n_recorded, n_scatt, max_tau_bits, n_steps;
     unsigned long long n_tracked, n_children, n_overflow, n_dropped;
     unsigned long long n_primaries, max_nstep, n_long, n_abandoned, abort, n_nan;
-    unsigned long long pad[2];
+    unsigned long long karg_bad; /* track_kernel's kernel-argument check failed (see kargs_check) */
+    unsigned long long pad;
 };
 static_assert(sizeof(DevCounters) == 16 * 8, "DevCounters layout (grm_engine_debug_counters)");
 
@@ -141,6 +142,7 @@ struct Ctl {
     unsigned long long *early_ready, early_cap, early_tag;
     unsigned long long *early_tail, *early_head, *early_done, *wg_exit, *early_live, *bulk_live;
     int early_steps;
+    int karg_test; /* test only (GRM_OPT_KARG_TEST): the kernel-argument check expects lanes + this */
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -859,6 +861,23 @@ __device__ __forceinline__ KArgsK *karg_fresh(KArgsK *ka) {
 }
 __device__ __forceinline__ const Params &karg_params(KArgsK *k) { return *(const Params *)&k->P; }
 __device__ __forceinline__ const Ctl &karg_ctl(KArgsK *k) { return *(const Ctl *)&k->C; }
+/* Guard of the kernarg-segment reads: the words the loop reads through kargs() must be the launch's
+ * arguments.  Compares, at the ends and in the middle of both blocks, the segment's words with the
+ * by-value parameters (which the compiler reads from the segment by its own ABI).  A layout the
+ * struct KArgs does not describe (a compiler or ABI change) makes this fail for every wave, and the
+ * launch then exits at once with DevCounters::karg_bad set, which the host turns into an error
+ * (run_passes): there is no silent wrong-argument mode.  Wave-uniform (scalar loads only). */
+__device__ __forceinline__ bool kargs_check(KArgsK *ka, const Params &P, const Ctl &C) {
+    const Params &kp = karg_params(ka);
+    const Ctl &kc = karg_ctl(ka);
+    bool ok = kp.n1 == P.n1 && kp.n2 == P.n2 && __double_as_longlong(kp.a) == __double_as_longlong(P.a) &&
+              __double_as_longlong(kp.bias_norm) == __double_as_longlong(P.bias_norm) && kp.zones == P.zones &&
+              kp.k2 == P.k2;
+    ok = ok && kc.pool == C.pool && kc.n_pool == C.n_pool && kc.ctr == C.ctr && kc.key0 == C.key0 &&
+         kc.spec_blocks == C.spec_blocks && kc.watchdog_ticks == C.watchdog_ticks && kc.lanes == C.lanes + C.karg_test &&
+         kc.early_steps == C.early_steps;
+    return __builtin_amdgcn_readfirstlane((int)ok) != 0;
+}
 
 /* The geometry wave of a pair (see above): runs photon after photon -- each begins as a restart
  * request from the interaction wave -- until LONE_STOP. */
@@ -1676,10 +1695,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     L.rng.k0 = C0.key0;
     L.rng.k1 = C0.key1;
     bool active = false;
-    bool pool_done = false;      /* wave-uniform */
+    /* a failed argument check ends the wave at its first trip (the exit path uses C0 only) */
+    const bool karg_bad = !kargs_check(ka, P0, C0);
+    if (karg_bad && lane_id == 0) atomicAdd(&C0.ctr->karg_bad, 1ull);
+    bool pool_done = karg_bad;   /* wave-uniform */
     unsigned long long res_next = 0, res_end = 0; /* wave-uniform: reserved claim positions */
     bool head_done = false;      /* wave-uniform: the pool head has passed pos_end */
-    bool warm = C0.admit_n != 0;  /* wave-uniform: warm-up admission in force */
+    bool warm = !karg_bad && C0.admit_n != 0; /* wave-uniform: warm-up admission in force */
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
     L.flight() = 0;
     /* wave-uniform; refreshed every trip during the warm-up and every REFRESH_TRIPS trips after it
@@ -1892,8 +1914,10 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
          * a step (one lane-loop trip is ~7 us per step for it, the pair ~1.8 us) */
         if (C.early_q && !warm) {
             const bool early = active && L.phase == 0 && L.n_step >= C.early_steps;
+            /* a full queue is read, not claimed: past early_cap every such lane would add to the one
+             * tail word on every trip for the rest of the launch */
             if (__ballot(early) && __hip_atomic_load(C.early_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT) == 1 &&
-                early) {
+                __hip_atomic_load(C.early_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < C.early_cap && early) {
                 const unsigned long long slot = atomicAdd(C.early_tail, 1ull);
                 if (slot < C.early_cap) {
                     export_lone(C.early_q + slot, L, cold);
@@ -2132,6 +2156,7 @@ struct grm_engine {
     /* early hand-over of long photons to early_kernel on a second stream (GRM_OPT_EARLY_STEPS) */
     int early_steps = 5000;
     bool early_serial = false; /* test: the worker ahead of the main launch on its stream */
+    int karg_test = 0;         /* test: GRM_OPT_KARG_TEST */
     static constexpr unsigned long long EARLY_CAP = 1024;
     LoneRec *d_early = nullptr;
     unsigned long long *d_early_ready = nullptr;
@@ -2291,6 +2316,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.lone_cap = e->lone_cap;
     C.lone_count = e->d_small + 7;
     C.lone_all = e->lone == 2;
+    C.karg_test = e->karg_test;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
@@ -2428,6 +2454,12 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         steps_pass = hp.n_steps;
         e->stats.n_launches++;
         e->stats.n_nan_photons = hp.n_nan;
+        if (hp.karg_bad) {
+            e->err = "track_kernel: the kernel-argument segment does not hold the launch's arguments in the "
+                     "layout of struct KArgs (" + std::to_string(hp.karg_bad) +
+                     " waves); no photon was tracked -- results of this call are invalid";
+            return -1;
+        }
         if (hp.abort) {
             e->stats.n_abandoned = hp.n_abandoned;
             e->err = "watchdog: a transport launch ran longer than " + std::to_string(e->watchdog_ms) + " ms; " +
@@ -2610,6 +2642,7 @@ void grm_engine_destroy(grm_engine *e) {
     if (!e) return;
     hipSetDevice(e->device);
     if (e->stream) hipStreamSynchronize(e->stream);
+    if (e->stream2) hipStreamSynchronize(e->stream2); /* early_kernel uses d_small, d_ctr, d_early ... */
     hipFree(e->d_zones);
     hipFree(e->d_hot);
     hipFree(e->d_k2);
@@ -2681,6 +2714,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
+    case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }
@@ -3028,6 +3062,43 @@ int grm_engine_stash_read(grm_engine *e, int slot, grm_spectrum_cell *spec, uint
     if (n_steps) *n_steps = sums[2];
     if (max_tau) std::memcpy(max_tau, &maxs[0], sizeof(double));
     return 0;
+}
+
+int grm_engine_stash_raw(grm_engine *e, int first, int n_slots, double *spec, uint64_t *sums, uint64_t *maxs,
+                         int write) {
+    if (!e) return -1;
+    if (first < 0 || n_slots < 0 || first + n_slots > e->stash_cap) {
+        e->err = "grm_engine_stash_raw: slots outside the reserved stash";
+        return -1;
+    }
+    if (n_slots == 0) return 0;
+    HIPCHK(e, hipSetDevice(e->device));
+    const size_t ncell = (size_t)N_TH_BINS * N_E_BINS * (sizeof(grm_spectrum_cell) / sizeof(double));
+    const hipMemcpyKind k = write ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+    struct Part {
+        void *dev, *host;
+        size_t bytes;
+    } parts[3] = {{e->d_stash_spec + (size_t)first * ncell, spec, (size_t)n_slots * ncell * sizeof(double)},
+                  {e->d_stash_sum + (size_t)first * STASH_SUMS, sums, (size_t)n_slots * STASH_SUMS * sizeof(uint64_t)},
+                  {e->d_stash_max + (size_t)first * STASH_MAXS, maxs, (size_t)n_slots * STASH_MAXS * sizeof(uint64_t)}};
+    for (const Part &q : parts) {
+        if (!q.host) continue;
+        if (write)
+            HIPCHK(e, hipMemcpyAsync(q.dev, q.host, q.bytes, k, e->stream));
+        else
+            HIPCHK(e, hipMemcpyAsync(q.host, q.dev, q.bytes, k, e->stream));
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int grm_stash_words(int which) {
+    switch (which) {
+    case 0: return N_TH_BINS * N_E_BINS * (int)(sizeof(grm_spectrum_cell) / sizeof(double));
+    case 1: return STASH_SUMS;
+    case 2: return STASH_MAXS;
+    default: return -1;
+    }
 }
 
 int grm_probe(grm_engine *e, int which, const double *in, int in_stride, double *out, int out_stride, size_t n) {

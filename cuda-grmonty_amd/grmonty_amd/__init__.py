@@ -52,6 +52,7 @@ OPT_LONE = 13
 OPT_WARMUP_BATCH = 14
 OPT_EARLY_STEPS = 15
 OPT_EARLY_SERIAL = 16
+OPT_KARG_TEST = 17
 N_TH_BINS, N_E_BINS = 6, 200
 
 
@@ -128,6 +129,8 @@ SIGNATURES = {
     "grm_engine_allreduce_stash": (C.c_int, [VP, C.c_int]),
     "grm_engine_stash_read": (C.c_int, [VP, C.c_int, VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "grm_engine_stash_raw": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, VP, C.c_int]),
+    "grm_stash_words": (C.c_int, [C.c_int]),
     "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
     "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_stuck": (C.c_int64, [VP, VP, C.c_size_t]),
@@ -400,7 +403,8 @@ class Engine:
         f = lambda b: float(np.array([b], dtype=np.uint64).view(np.float64)[0])  # noqa: E731
         return {"n_recorded": v[0], "n_scatt": v[1], "max_tau_scatt": f(v[2]), "n_steps": v[3],
                 "n_tracked": v[4], "n_children": v[5], "n_overflow": v[6], "n_dropped": v[7], "n_primaries": v[8],
-                "max_photon_steps": v[9], "n_long": v[10], "n_abandoned": v[11], "n_nan": v[13]}
+                "max_photon_steps": v[9], "n_long": v[10], "n_abandoned": v[11], "n_nan": v[13],
+                "karg_bad": v[14]}
 
     def allreduce(self):
         self._check(self.L.grm_engine_allreduce(self.h))
@@ -422,6 +426,23 @@ class Engine:
         self._check(self.L.grm_engine_stash_read(self.h, int(slot), _ptr(spec), C.byref(nr), C.byref(ns), C.byref(mt),
                                                  C.byref(st)))
         return spec.reshape(N_TH_BINS, N_E_BINS), nr.value, ns.value, mt.value, st.value
+
+    def stash_raw(self, n_slots: int, first: int = 0):
+        """(spectra [n, words0] f64, sums [n, words1] u64, maxs [n, words2] u64): the stash's raw
+        words in the engine's packing (grm_engine_stash_raw)"""
+        w = [self.L.grm_stash_words(i) for i in range(3)]
+        spec = np.zeros((n_slots, w[0]))
+        sums = np.zeros((n_slots, w[1]), dtype=np.uint64)
+        maxs = np.zeros((n_slots, w[2]), dtype=np.uint64)
+        self._check(self.L.grm_engine_stash_raw(self.h, int(first), int(n_slots), _ptr(spec), _ptr(sums), _ptr(maxs), 0))
+        return spec, sums, maxs
+
+    def stash_raw_write(self, spec: np.ndarray, sums: np.ndarray, maxs: np.ndarray, first: int = 0):
+        spec = np.ascontiguousarray(spec, dtype=np.float64)
+        sums = np.ascontiguousarray(sums, dtype=np.uint64)
+        maxs = np.ascontiguousarray(maxs, dtype=np.uint64)
+        self._check(self.L.grm_engine_stash_raw(self.h, int(first), int(spec.shape[0]), _ptr(spec), _ptr(sums),
+                                                _ptr(maxs), 1))
 
     def probe(self, which: int, inputs: np.ndarray, out_width: int) -> np.ndarray:
         a = np.ascontiguousarray(inputs, dtype=np.float64)

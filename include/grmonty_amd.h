@@ -167,7 +167,10 @@ enum {
     GRM_OPT_EARLY_STEPS = 15,
     /* test only: 1 launches the early worker on the transport stream ahead of the main launch, as a
      * kernel-serialising tool (a counter profiler) would run them; the worker must then leave */
-    GRM_OPT_EARLY_SERIAL = 16
+    GRM_OPT_EARLY_SERIAL = 16,
+    /* test only: != 0 makes the transport kernel's kernel-argument check fail (the failure path must
+     * end the call with an error, no photon tracked) */
+    GRM_OPT_KARG_TEST = 17
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
@@ -215,7 +218,7 @@ int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap);
 int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap);
 /* raw device counters: n_recorded, n_scatt, max_tau_scatt bits, n_steps, n_tracked, n_children,
  * n_overflow, n_dropped, n_primaries, max photon steps, lives > 1e5 steps, n_abandoned, abort, n_nan,
- * 2 reserved */
+ * waves whose kernel-argument check failed, 1 reserved */
 int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]);
 
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
@@ -237,6 +240,15 @@ int grm_engine_stash(grm_engine *e, int slot);
 int grm_engine_allreduce_stash(grm_engine *e, int n_slots);
 int grm_engine_stash_read(grm_engine *e, int slot, grm_spectrum_cell *spec, uint64_t *n_rec, uint64_t *n_scatt,
                           double *max_tau, uint64_t *n_steps);
+/* The stash's raw words of slots [first, first + n_slots), in the engine's own packing, read
+ * (write = 0) or written back (write = 1): per slot grm_stash_words(0) spectrum doubles (reduced by
+ * sum), grm_stash_words(1) u64 words reduced by sum (recorded, scattered, steps, tracked, children,
+ * overflow, dropped, primaries, lives > 1e5 steps) and grm_stash_words(2) reduced by max (max
+ * tau_scatt bits, longest life).  A null array skips its part.  For a reduction over another
+ * transport than RCCL (tests: gloo) with exactly grm_engine_allreduce_stash's semantics. */
+int grm_engine_stash_raw(grm_engine *e, int first, int n_slots, double *spec, uint64_t *sums, uint64_t *maxs,
+                         int write);
+int grm_stash_words(int which);
 
 /* --- host model (harm_model.hpp; C++ host, no GPU) ------------------------------------- */
 typedef struct grm_model grm_model;

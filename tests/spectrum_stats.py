@@ -39,3 +39,13 @@ def binned_ks(c1, c2, theta=None):
 
 def ks_crit(n1, n2, alpha=1e-3):
     return C_ALPHA[alpha] * np.sqrt((n1 + n2) / (n1 * n2))
+
+
+def welch_z(dev, ref):
+    """(difference of the means, its combined standard error, z): the device runs' mean against the
+    oracle runs' mean, each with its own sample variance (Welch)"""
+    dev = np.asarray(dev, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    se = np.sqrt(dev.var(ddof=1) / len(dev) + ref.var(ddof=1) / len(ref))
+    diff = dev.mean() - ref.mean()
+    return diff, se, diff / se

@@ -5,6 +5,11 @@
    (:1066, record_super_photon :1291-1295), so ending it early is output-equivalent.
 2. The per-launch watchdog (GRM_OPT_WATCHDOG_MS) abandons a launch that runs too long, reports it as
    an error with the abandoned photons' state, and the engine stays usable afterwards.
+3. The kernel-argument guard of track_kernel (kargs_check, grm_engine.hip): the launch's arguments
+   are read in the loop through the kernarg segment laid out as struct KArgs; every wave compares
+   that view with the by-value parameters at entry.  A normal call reports it clean; with the
+   failure injected (GRM_OPT_KARG_TEST) the call fails with the reason, tracks nothing, and the
+   engine is usable afterwards.
 """
 import numpy as np
 import pytest
@@ -66,3 +71,26 @@ def test_watchdog_abandons_and_recovers(model64):
     eng.track(ph[np.random.default_rng(1).permutation(len(ph))[:4000]])
     _, nr, _, _ = eng.finish()
     assert eng.stats()["n_abandoned"] == 0 and nr > 0
+
+
+def test_kernel_argument_guard(model64):
+    import grmonty_amd as G
+    ph = model64.emit(seed=123)[:3000]
+    eng = G.Engine(model64, device=0)
+    _frozen(G, eng)
+    eng.track(ph)
+    assert eng.debug_counters()["karg_bad"] == 0
+    _, nr0, _, _ = eng.finish()
+    assert nr0 > 0
+    _frozen(G, eng)
+    eng.set_option(G.OPT_KARG_TEST, 1)
+    with pytest.raises(RuntimeError, match="kernel-argument"):
+        eng.track(ph)
+    c = eng.debug_counters()
+    assert c["karg_bad"] > 0 and c["n_steps"] == 0 and c["n_tracked"] == 0
+    eng.set_option(G.OPT_KARG_TEST, 0)
+    _frozen(G, eng)
+    eng.track(ph)
+    _, nr1, _, _ = eng.finish()
+    assert nr1 == nr0 and eng.debug_counters()["karg_bad"] == 0
+    eng.close()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the transport kernel of an earlier git revision as an A/B variant:
-#   tools/build_rev.sh <rev> <name>  ->  cuda-grmonty_amd/variants/libgrmonty_amd_v<name>.so
+#   tools/build_rev.sh <rev> <name>  ->  cuda-grmonty_amd/ab/libgrmonty_amd_v<name>.so
 # (kernel sources of <rev>, current host objects; only for revisions with the same C ABI)
 set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
@@ -23,7 +23,7 @@ for f in grm_probe grm_emit grm_tables; do
   objs="$objs $D/$f.o"
 done
 wait
-mkdir -p "$R/cuda-grmonty_amd/variants"
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/cuda-grmonty_amd/variants/libgrmonty_amd_v$name.so" \
+mkdir -p "$R/cuda-grmonty_amd/ab"
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/cuda-grmonty_amd/ab/libgrmonty_amd_v$name.so" \
   $objs "$R/cuda-grmonty_amd/build/grm_host.o" -L/opt/rocm/lib -lrccl -lpthread
-echo "built variants/libgrmonty_amd_v$name.so from $rev"
+echo "built ab/libgrmonty_amd_v$name.so from $rev"

@@ -1,15 +1,15 @@
 #!/bin/bash
 # Build the working tree's kernels with extra engine flags as an A/B variant:
-#   [SCHED=none|max-ilp|...] VFLAGS="-DX=1" tools/build_variant.sh <name>  ->  cuda-grmonty_amd/variants/libgrmonty_amd_v<name>.so
+#   [SCHED=none|max-ilp|...] VFLAGS="-DX=1" tools/build_variant.sh <name>  ->  cuda-grmonty_amd/ab/libgrmonty_amd_v<name>.so
 set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 name=$1
-D="$R/cuda-grmonty_amd/build/var_$name"; mkdir -p "$D" "$R/cuda-grmonty_amd/variants"
+D="$R/cuda-grmonty_amd/build/var_$name"; mkdir -p "$D" "$R/cuda-grmonty_amd/ab"
 make -s -C "$R/cuda-grmonty_amd" build/grm_host.o build/grm_probe.o build/grm_emit.o build/grm_tables.o
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -mllvm -disable-machine-licm"
 SCHED=${SCHED:-none}; SF=""; [ "$SCHED" = none ] || SF="-mllvm -amdgpu-sched-strategy=$SCHED"
 /opt/rocm/bin/hipcc $FL $SF $VFLAGS -c "$R/cuda-grmonty_amd/csrc/grm_engine.hip" -o "$D/grm_engine.o"
 B="$R/cuda-grmonty_amd/build"
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/cuda-grmonty_amd/variants/libgrmonty_amd_v$name.so" \
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/cuda-grmonty_amd/ab/libgrmonty_amd_v$name.so" \
   "$D/grm_engine.o" $B/grm_probe.o $B/grm_emit.o $B/grm_tables.o $B/grm_host.o -L/opt/rocm/lib -lrccl -lpthread
-echo "built variants/libgrmonty_amd_v$name.so ($VFLAGS)"
+echo "built ab/libgrmonty_amd_v$name.so ($VFLAGS)"

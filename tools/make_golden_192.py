@@ -11,7 +11,9 @@ and commits, per seed:
 and the full 6x200x13 spectrum of seed 123 (writer fixtures).
 Output: tests/golden/oracle_synth192_pn1e5.npz (+ .json summary).  Takes ~5 min on 6 cores.
 
-    python tools/make_golden_192.py [--seeds 123,124,125,126,127,128] [--photon-n 1e5]
+    python tools/make_golden_192.py [--seeds 123,124,125,126,127,128] [--photon-n 1e5] [--merge]
+
+--merge adds the new seeds' runs to the committed fixtures (seeds already there are skipped).
 """
 import argparse
 import json
@@ -58,14 +60,26 @@ def main():
     ap.add_argument("--seeds", default="123,124,125,126,127,128")
     ap.add_argument("--photon-n", type=float, default=1e5)
     ap.add_argument("--grid", type=int, default=192)
+    ap.add_argument("--merge", action="store_true", help="append to the committed fixtures")
     args = ap.parse_args()
     from grmonty_amd.synth_dump import ensure_dump
     path = ensure_dump(os.path.join("/tmp", f"synth{args.grid}.dump"), args.grid, args.grid)
     seeds = [int(s) for s in args.seeds.split(",")]
+    old = []
+    if args.merge:
+        g = np.load(OUT + ".npz")
+        js = json.load(open(OUT + ".json"))
+        for i, r in enumerate(js["runs"]):
+            old.append(dict(seed=r["seed"], wall_s=r["wall_s"], luminosity=r["luminosity"],
+                            max_tau_scatt=r["max_tau_scatt"], cells=g["cells"][i],
+                            counters={k: r[k] for k in ("created", "scattered", "recorded", "steps")},
+                            spectrum=g["spectrum123"] if r["seed"] == 123 else None))
+        seeds = [s for s in seeds if s not in {r["seed"] for r in old}]
     t = time.time()
-    with mp.Pool(len(seeds)) as pool:
+    with mp.Pool(max(1, len(seeds))) as pool:
         res = pool.map(run, [(path, int(args.photon_n), s) for s in seeds])
     print(f"{len(seeds)} oracle runs in {time.time() - t:.0f} s")
+    res = old + res
     res.sort(key=lambda r: r["seed"])
     spec = next(r["spectrum"] for r in res if r["spectrum"] is not None)
     np.savez_compressed(OUT + ".npz", seeds=np.array(seeds), cells=np.stack([r["cells"] for r in res]),
