@@ -23,9 +23,11 @@ own streams and buffers, distinct seeds) -- device throughput when independent r
 it is NOT value.
 
 Multi-GPU: one process per GPU.  --scaling weak (default): the job is photon_n x N, zone-sharded
-into N contiguous ranges of equal expected photon count; --scaling strong: the job is photon_n,
-zone-sharded the same way.  Zone emission streams and photon ids are global, so the union of the
-shards is exactly the single-GPU job's photon list.  The only exchange is the end-of-pass RCCL
+over the N ranks, rank r taking every N-th zone from zone r (grmonty_amd.zone_shards "strided": each
+rank's adaptive bias then sees a history of the whole disk; contiguous ranges moved the counters by
++17..+43 %); --scaling strong: the job is photon_n, zone-sharded the same way.  Zone
+emission streams are keyed by zone and photon ids are global (rank r's id base = the photons of the
+ranks before it), so the union of the shards is exactly the single-GPU job's photon set.  The only exchange is the end-of-pass RCCL
 all-reduce (xGMI) of the 6x200x13 fp64 spectrum + counters, one communicator per rank, issued by the
 engine's C library on its stream.  torch.distributed runs with the gloo backend only (rendezvous,
 RCCL unique-id broadcast, barriers, max-over-ranks timing): torch's own HIP runtime is never
@@ -199,15 +201,15 @@ def main():
     t = time.time()
     model = G.Model.load(path, photon_n=photon_n_job).init(threads, device=local)
     t_init = time.time() - t
-    shards = G.shard_zones(model.zone_weights(), world)
-    z0, z1 = shards[rank]
+    shards = G.zone_shards(model.zone_weights(), world, "strided")
+    z0, z1, zst = shards[rank]
     timed_seeds = [SEED0 + s for s in range(args.steps)]
     warm_seeds = [WARM_SEED0 + s for s in range(args.warmup)]
     # per-seed photon counts of every shard (host, outside the timing): the rank's id base
     t = time.time()
     id_base = {}
     for sd in warm_seeds + timed_seeds:
-        id_base[sd] = sum(model.count(seed=sd, z0=a, z1=b, threads=threads) for a, b in shards[:rank])
+        id_base[sd] = sum(model.count(seed=sd, z0=a, z1=b, threads=threads, stride=st) for a, b, st in shards[:rank])
     t_count = time.time() - t
     engine = G.Engine(model, device=local)
     # A/B hook: GRM_BENCH_OPTS="15=2000,9=2" sets engine options (grmonty_amd.OPT_*) before the passes
@@ -226,7 +228,7 @@ def main():
         eng.reset()
         eng.set_option(G.OPT_SEED, seed)
         eng.set_option(G.OPT_ID_BASE, base)
-        ptr, n_dev = eng.emit(seed=seed, z0=z0, z1=z1)
+        ptr, n_dev = eng.emit(seed=seed, z0=z0, z1=z1, stride=zst)
         eng.track_device(ptr, n_dev)
         st = eng.stats()
         if slot is not None:
@@ -297,7 +299,7 @@ def main():
 
     overlapped = None
     if rank == 0 and overlap > 1:
-        overlapped = overlapped_throughput(model, overlap, z0, z1)
+        overlapped = overlapped_throughput(model, overlap, z0, z1, zst)
     if rank == 0:
         sts = [r[1] for r in res]
         launches = res[-1][1]["n_launches"] - launches0
@@ -314,7 +316,7 @@ def main():
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             try:
-                ph = model.emit(seed=SEED0, z0=z0, z1=z1, threads=threads)
+                ph = model.emit(seed=SEED0, z0=z0, z1=z1, threads=threads, stride=zst)
                 cpu = cpu_baseline(path, photon_n_job, ph, args.cpu_seconds)
             except Exception as ex:  # the baseline is reported beside the product, never part of it
                 cpu = {"value": None, "error": repr(ex)}
@@ -337,7 +339,7 @@ def main():
                                    f"mass_unit=4e19, zone-sharded over {world} GPU(s)",
                        "photon_n_job": photon_n_job, "grid": f"{args.grid}x{args.grid}",
                        "superphotons_per_pass_rank0": n_rank // max(1, args.steps),
-                       "parallelism": f"zone shards x{world}" + (", passes stashed on the device, one RCCL all-reduce per job"
+                       "parallelism": f"strided zone shards x{world}" + (", passes stashed on the device, one RCCL all-reduce per job"
                                                                   if world > 1 else "")},
             "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": achieved_tf / FP64_PEAK_TFS if achieved_tf else None,
@@ -372,7 +374,7 @@ def main():
         dist.destroy_process_group()
 
 
-def overlapped_throughput(model, jobs: int, z0: int, z1: int):
+def overlapped_throughput(model, jobs: int, z0: int, z1: int, zst: int = 1):
     """detail only: `jobs` independent passes (distinct seeds) in flight at once, one engine + host
     thread each, on this rank's zones -- what the device sustains when runs share it"""
     import threading
@@ -387,7 +389,7 @@ def overlapped_throughput(model, jobs: int, z0: int, z1: int):
             e.reset()
             e.set_option(G.OPT_SEED, seed)
             e.set_option(G.OPT_ID_BASE, 0)
-            ptr, n = e.emit(seed=seed, z0=z0, z1=z1)
+            ptr, n = e.emit(seed=seed, z0=z0, z1=z1, stride=zst)
             e.track_device(ptr, n)
             st = e.stats()
             if st["n_dropped"] or st["n_abandoned"]:

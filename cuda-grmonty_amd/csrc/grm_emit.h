@@ -25,8 +25,8 @@ struct EmitParams {
 
 } /* namespace grm */
 
-/* zone counts + scan of zones [z0, z0 + n_zones), then one lane per photon into *out (grown to
- * fit; *out_cap updated); d_off holds n_zones + 1 offsets.  Synchronous; 0 = OK. */
-int grm_emit_launch(const grm::Params &P, const grm::EmitParams &E, uint64_t z0, uint64_t n_zones,
+/* zone counts + scan of zones z0 + q * stride, q in [0, n_zones), then one lane per photon into
+ * *out (grown to fit; *out_cap updated); d_off holds n_zones + 1 offsets.  Synchronous; 0 = OK. */
+int grm_emit_launch(const grm::Params &P, const grm::EmitParams &E, uint64_t z0, uint64_t stride, uint64_t n_zones,
                     unsigned long long *d_off, hipStream_t s, unsigned long long *h_total, grm_init_photon **out,
                     size_t *out_cap, uint64_t *n_out, std::string &err);

@@ -55,15 +55,17 @@ __device__ __forceinline__ uint32_t zone_count(const grm_emit_zone *zones, uint6
     return (fmod(nz, 1.0) > u) ? (uint32_t)((int)nz + 1) : (uint32_t)(int)nz;
 }
 
-/* counts of zones [z0, z0 + n) and their exclusive prefix sum off[0..n] (one workgroup; each
- * thread owns a contiguous chunk and recomputes its counts in the second pass instead of storing) */
-__global__ __launch_bounds__(SCAN_THREADS) void zone_count_scan(const grm_emit_zone *zones, uint64_t z0, uint64_t n,
-                                                                uint32_t k0, uint32_t k1, unsigned long long *off, unsigned long long *h_total) {
+/* counts of zones z0 + q * stride, q in [0, n), and their exclusive prefix sum off[0..n] (one
+ * workgroup; each thread owns a contiguous chunk and recomputes its counts in the second pass
+ * instead of storing) */
+__global__ __launch_bounds__(SCAN_THREADS) void zone_count_scan(const grm_emit_zone *zones, uint64_t z0, uint64_t stride,
+                                                                uint64_t n, uint32_t k0, uint32_t k1, unsigned long long *off,
+                                                                unsigned long long *h_total) {
     __shared__ unsigned long long part[SCAN_THREADS];
     const uint64_t per = (n + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint64_t a = min(n, (uint64_t)threadIdx.x * per), b = min(n, a + per);
     unsigned long long s = 0;
-    for (uint64_t q = a; q < b; ++q) s += zone_count(zones, z0 + q, k0, k1);
+    for (uint64_t q = a; q < b; ++q) s += zone_count(zones, z0 + q * stride, k0, k1);
     part[threadIdx.x] = s;
     __syncthreads();
     /* Hillis-Steele inclusive scan of the 1024 chunk sums */
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void zone_count_scan(const grm_emit_z
     unsigned long long run = part[threadIdx.x] - s;
     for (uint64_t q = a; q < b; ++q) {
         off[q] = run;
-        run += zone_count(zones, z0 + q, k0, k1);
+        run += zone_count(zones, z0 + q * stride, k0, k1);
     }
     if (threadIdx.x == SCAN_THREADS - 1) {
         off[n] = part[SCAN_THREADS - 1];
@@ -155,9 +157,9 @@ __device__ void sample_photon(const Params &P, const EmitParams &E, const grm_em
     ph.pad_ = 0;
 }
 
-__global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(Params P, EmitParams E, uint64_t z0, uint64_t n_zones,
-                                                          const unsigned long long *off, uint64_t total,
-                                                          grm_init_photon *out) {
+__global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(Params P, EmitParams E, uint64_t z0, uint64_t stride,
+                                                          uint64_t n_zones, const unsigned long long *off,
+                                                          uint64_t total, grm_init_photon *out) {
     const uint64_t g = (uint64_t)blockIdx.x * EMIT_BLOCK + threadIdx.x;
     if (g >= total) return;
     /* zone q with off[q] <= g < off[q + 1] (empty zones have off[q] == off[q + 1]) */
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(Params P, EmitParams E
         else
             hi = mid;
     }
-    const uint64_t z = z0 + lo;
+    const uint64_t z = z0 + lo * stride;
     const grm_emit_zone &Z = E.zones[z];
     Rng r = zone_rng(E.k0, E.k1, z, g - off[lo] + 1);
     grm_init_photon ph;
@@ -183,7 +185,8 @@ __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(Params P, EmitParams E
 
 } /* namespace */
 
-int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t n_zones, unsigned long long *d_off,
+int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t stride, uint64_t n_zones,
+                    unsigned long long *d_off,
                     hipStream_t s, unsigned long long *h_total, grm_init_photon **out, size_t *out_cap, uint64_t *n_out,
                     std::string &err) {
     auto chk = [&](hipError_t st, const char *what) {
@@ -194,8 +197,8 @@ int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t 
     *n_out = 0;
     if (n_zones == 0) return 0;
     /* h_total: a host-mapped word the scan kernel writes itself (no copy kernel on the stream) */
-    hipLaunchKernelGGL(zone_count_scan, dim3(1), dim3(SCAN_THREADS), 0, s, E.zones, z0, n_zones, E.k0, E.k1, d_off,
-                       h_total);
+    hipLaunchKernelGGL(zone_count_scan, dim3(1), dim3(SCAN_THREADS), 0, s, E.zones, z0, stride, n_zones, E.k0, E.k1,
+                       d_off, h_total);
     if (!chk(hipGetLastError(), "zone_count_scan") || !chk(hipStreamSynchronize(s), "sync")) return -1;
     const unsigned long long total = *(volatile unsigned long long *)h_total;
     if (total > *out_cap) {
@@ -211,8 +214,8 @@ int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t 
             err = "emit: too many photons for one launch";
             return -1;
         }
-        hipLaunchKernelGGL(emit_kernel, dim3((unsigned)blocks), dim3(EMIT_BLOCK), 0, s, P, E, z0, n_zones, d_off,
-                           (uint64_t)total, *out);
+        hipLaunchKernelGGL(emit_kernel, dim3((unsigned)blocks), dim3(EMIT_BLOCK), 0, s, P, E, z0, stride, n_zones,
+                           d_off, (uint64_t)total, *out);
         if (!chk(hipGetLastError(), "emit_kernel") || !chk(hipStreamSynchronize(s), "emit sync")) return -1;
     }
     *n_out = total;

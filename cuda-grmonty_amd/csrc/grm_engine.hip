@@ -364,6 +364,11 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
                 atomicAdd(cnt + 1, (unsigned long long)n_scatt);
                 double *s = spec + (ix2 * N_E_BINS + i_e) * cell_stride;
                 const double x1i = cold->x1i, x2i = cold->x2i;
+#ifdef GRM_X_NOSPEC /* experiment only: the cost of the spectrum atomics (results wrong) */
+                if (cell_stride == SPEC_FIELDS) s = nullptr;
+                if (s)
+#endif
+                {
                 atomicAdd(s + 0, w);                      /* dn_dle */
                 atomicAdd(s + 1, w * e);                  /* de_dle */
                 atomicAdd(s + 2, 1.0);                    /* nph */
@@ -376,6 +381,7 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
                 atomicAdd(s + 9, w * cold->n_e_0);        /* ne_0 */
                 atomicAdd(s + 10, w * cold->theta_e_0);   /* theta_e_0 */
                 atomicAdd(s + 11, w * cold->b_0);         /* b_0 */
+                }
             } else {
                 i_e = -1;
             }
@@ -2839,7 +2845,16 @@ int grm_engine_emit_setup(grm_engine *e, const grm_emit_zone *zones, int64_t n_z
 
 int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon **dev_out,
                     uint64_t *n_out) {
+    return grm_engine_emit_strided(e, seed, z0, z1, 1, dev_out, n_out);
+}
+
+int grm_engine_emit_strided(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, int64_t stride,
+                            grm_init_photon **dev_out, uint64_t *n_out) {
     if (!e || !dev_out || !n_out) return -1;
+    if (stride < 1) {
+        e->err = "grm_engine_emit_strided: stride < 1";
+        return -1;
+    }
     if (!e->d_ezones) {
         e->err = "grm_engine_emit: no zone table (grm_engine_emit_setup)";
         return -1;
@@ -2848,6 +2863,7 @@ int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_in
     if (z1 < 0 || z1 > e->n_ezones) z1 = e->n_ezones;
     if (z0 < 0) z0 = 0;
     if (z0 > z1) z0 = z1;
+    const uint64_t n_zones = (uint64_t)((z1 - z0 + stride - 1) / stride);
     /* consts.hpp:33-157 emission constants, host libm like the host model's */
     EmitParams E;
     E.zones = e->d_ezones;
@@ -2863,8 +2879,8 @@ int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_in
     E.k1 = (uint32_t)(seed >> 32);
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     uint64_t n = 0;
-    if (grm_emit_launch(e->P, E, (uint64_t)z0, (uint64_t)(z1 - z0), e->d_eoff, e->stream, &e->pin->word[4], &e->d_emit, &e->emit_cap,
-                        &n, e->err))
+    if (grm_emit_launch(e->P, E, (uint64_t)z0, (uint64_t)stride, n_zones, e->d_eoff, e->stream, &e->pin->word[4], &e->d_emit,
+                        &e->emit_cap, &n, e->err))
         return -1;
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     HIPCHK(e, hipEventSynchronize(e->ev1));

@@ -111,6 +111,7 @@ SIGNATURES = {
     "grm_model_table": (DP, [VP, C.c_int]),
     "grm_engine_create_from_model": (C.c_int, [VP, C.c_int, C.POINTER(VP)]),
     "grm_model_emit": (C.c_int64, [VP, C.c_uint64, C.c_int64, C.c_int64, VP, C.c_size_t, C.c_int]),
+    "grm_model_emit_strided": (C.c_int64, [VP, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, VP, C.c_size_t, C.c_int]),
     "grm_model_zone_weights": (C.c_int, [VP, DP]),
     "grm_write_spectrum": (C.c_int, [VP, VP, C.c_char_p, DP]),
     "grm_write_spectrum_stats": (C.c_int, [VP, VP, C.c_char_p]),
@@ -118,6 +119,8 @@ SIGNATURES = {
     "grm_engine_emit_setup": (C.c_int, [VP, VP, C.c_int64, DP, DP]),
     "grm_engine_emit_setup_from_model": (C.c_int, [VP, VP]),
     "grm_engine_emit": (C.c_int, [VP, C.c_uint64, C.c_int64, C.c_int64, C.POINTER(VP), C.POINTER(C.c_uint64)]),
+    "grm_engine_emit_strided": (C.c_int, [VP, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.POINTER(VP),
+                                          C.POINTER(C.c_uint64)]),
     "grm_engine_download": (C.c_int, [VP, VP, C.c_size_t, VP]),
     "grm_probe": (C.c_int, [VP, C.c_int, DP, C.c_int, DP, C.c_int, C.c_size_t]),
     "grm_engine_upload": (C.c_int, [VP, VP, C.c_size_t, C.POINTER(VP)]),
@@ -235,16 +238,17 @@ class Model:
             n = self.TABLE_SIZES[which]
         return np.ctypeslib.as_array(self.L.grm_model_table(self.h, which), shape=(n,)).copy()
 
-    def count(self, seed: int = 123, z0: int = 0, z1: int = -1, threads: int = 0) -> int:
-        n = self.L.grm_model_emit(self.h, seed, z0, z1, None, 0, threads)
+    def count(self, seed: int = 123, z0: int = 0, z1: int = -1, threads: int = 0, stride: int = 1) -> int:
+        n = self.L.grm_model_emit_strided(self.h, seed, z0, z1, stride, None, 0, threads)
         if n < 0:
             raise RuntimeError(self.L.grm_model_last_error().decode())
         return int(n)
 
-    def emit(self, seed: int = 123, z0: int = 0, z1: int = -1, threads: int = 0) -> np.ndarray:
-        n = self.count(seed, z0, z1, threads)
+    def emit(self, seed: int = 123, z0: int = 0, z1: int = -1, threads: int = 0, stride: int = 1) -> np.ndarray:
+        """the superphotons of zones z0, z0 + stride, ... < z1 (make_super_photon's zone walk)"""
+        n = self.count(seed, z0, z1, threads, stride)
         out = np.zeros(n, dtype=INIT_PHOTON)
-        got = self.L.grm_model_emit(self.h, seed, z0, z1, _ptr(out), n, threads)
+        got = self.L.grm_model_emit_strided(self.h, seed, z0, z1, stride, _ptr(out), n, threads)
         if got != n:
             raise RuntimeError(self.L.grm_model_last_error().decode())
         return out
@@ -318,11 +322,12 @@ class Engine:
             msg = self.L.grm_engine_last_error(self.h).decode() or self.L.grm_model_last_error().decode()
             raise RuntimeError(msg)
 
-    def emit(self, seed: int = 123, z0: int = 0, z1: int = -1) -> tuple[int, int]:
-        """Emit the superphotons of zones [z0, z1) on the GPU; returns (device address, count).
-        The buffer is engine-owned and valid until the next emit."""
+    def emit(self, seed: int = 123, z0: int = 0, z1: int = -1, stride: int = 1) -> tuple[int, int]:
+        """Emit the superphotons of zones z0, z0 + stride, ... < z1 on the GPU; returns (device
+        address, count).  The buffer is engine-owned and valid until the next emit."""
         p, n = VP(), C.c_uint64()
-        self._check(self.L.grm_engine_emit(self.h, int(seed), int(z0), int(z1), C.byref(p), C.byref(n)))
+        self._check(self.L.grm_engine_emit_strided(self.h, int(seed), int(z0), int(z1), int(stride), C.byref(p),
+                                                   C.byref(n)))
         return int(p.value or 0), int(n.value)
 
     def download(self, dev_ptr: int, n: int) -> np.ndarray:
@@ -468,6 +473,26 @@ def shard_zones(zone_weights: np.ndarray, world: int) -> list[tuple[int, int]]:
     for r in range(1, len(cuts)):
         cuts[r] = max(cuts[r], cuts[r - 1])
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def zone_shards(zone_weights: np.ndarray, world: int, mode: str = "strided") -> list[tuple[int, int, int]]:
+    """The multi-GPU partition of one run as (z0, z1, stride) zone sets, rank r's zones being
+    z0, z0 + stride, ... < z1.
+
+    "strided" (the default, bench.py's): rank r takes every world-th zone from zone r.  Each rank's
+    photons then sample the whole disk, so its adaptive bias (bias_func, harm_model.cpp:1391-1404,
+    driven by the counters of the photons IT recorded) sees the same mix of histories as one GPU
+    does.  "contiguous": shard_zones' ranges of equal expected count -- a rank of inner zones alone
+    records nothing and one of the escape region records 2-3x the average, which moved the job's
+    recorded / scattered counts +17 / +30 / +43 % at 2 / 4 / 8 ranks (tests/test_gpu_multirank.py,
+    DESIGN.md §7).  Either way zone streams are keyed by zone, so the union of the shards is exactly
+    the single-GPU photon set."""
+    n = len(zone_weights)
+    if mode == "strided":
+        return [(r, n, world) for r in range(world)]
+    if mode == "contiguous":
+        return [(a, b, 1) for a, b in shard_zones(zone_weights, world)]
+    raise ValueError(mode)
 
 
 def rccl_unique_id() -> bytes:

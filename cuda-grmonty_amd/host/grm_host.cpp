@@ -872,6 +872,11 @@ int grm_model_zone_weights(const grm_model *m, double *out) {
 
 int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon *out, size_t cap,
                        int n_threads) {
+    return grm_model_emit_strided(m, seed, z0, z1, 1, out, cap, n_threads);
+}
+
+int64_t grm_model_emit_strided(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, int64_t stride, grm_init_photon *out,
+                               size_t cap, int n_threads) {
     if (!m || !m->inited) {
         set_err("model not initialised");
         return -1;
@@ -880,13 +885,17 @@ int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_
     if (z1 < 0 || z1 > nz) z1 = nz;
     if (z0 < 0) z0 = 0;
     if (z0 >= z1) return 0;
+    if (stride < 1) {
+        set_err("emit: stride < 1");
+        return -1;
+    }
     if (n_threads < 1) n_threads = default_threads();
-    const int64_t n = z1 - z0;
+    const int64_t n = (z1 - z0 + stride - 1) / stride; /* zones z0 + q * stride */
     std::vector<int> cnt((size_t)n);
     const int CH = 256;
     parallel_for((int)((n + CH - 1) / CH), n_threads, [&](int c) {
         for (int64_t q = (int64_t)c * CH; q < std::min<int64_t>(n, (int64_t)(c + 1) * CH); ++q) {
-            const int64_t z = z0 + q;
+            const int64_t z = z0 + q * stride;
             cnt[(size_t)q] = zone_count(m, seed, (int)(z / m->n2()), (int)(z % m->n2()));
         }
     });
@@ -901,7 +910,7 @@ int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_
     parallel_for((int)((n + CH - 1) / CH), n_threads, [&](int c) {
         for (int64_t q = (int64_t)c * CH; q < std::min<int64_t>(n, (int64_t)(c + 1) * CH); ++q) {
             if (cnt[(size_t)q] == 0) continue;
-            const int64_t z = z0 + q;
+            const int64_t z = z0 + q * stride;
             grm_emit_zone r;
             zone_record(m, (int)(z / m->n2()), (int)(z % m->n2()), r);
             emit_zone(m, r, seed, (uint64_t)z, cnt[(size_t)q], out + off[(size_t)q]);

@@ -281,6 +281,10 @@ int grm_engine_create_from_model(const grm_model *m, int device, grm_engine **ou
  * (z1 < 0 = all) -- used to shard emission across ranks. */
 int64_t grm_model_emit(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon *out, size_t cap,
                        int n_threads);
+/* the same for the zones z0, z0 + stride, z0 + 2 stride, ... < z1 (a strided shard: rank r of N
+ * takes z0 = r, stride = N; the union over ranks is again exactly the single-GPU photon set) */
+int64_t grm_model_emit_strided(grm_model *m, uint64_t seed, int64_t z0, int64_t z1, int64_t stride, grm_init_photon *out,
+                               size_t cap, int n_threads);
 /* cumulative expected photon count per zone, for balanced zone-range sharding (n1*n2 doubles) */
 int grm_model_zone_weights(const grm_model *m, double *out);
 
@@ -313,6 +317,9 @@ int grm_engine_emit_setup_from_model(grm_engine *e, const grm_model *m);
  * buffer valid until the next emit or destroy; synchronous. */
 int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_init_photon **dev_out,
                     uint64_t *n_out);
+/* the zones z0, z0 + stride, ... < z1 (grm_model_emit_strided's set, the same photons) */
+int grm_engine_emit_strided(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, int64_t stride,
+                            grm_init_photon **dev_out, uint64_t *n_out);
 /* device -> host copy of n photons from an engine buffer (tests, writers) */
 int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm_init_photon *host_out);
 

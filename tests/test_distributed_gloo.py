@@ -52,9 +52,10 @@ def _shard_job(rank, world, dump, out_dir, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     model = G.Model.load(dump, photon_n=150 * world).init(2)
-    shards = G.shard_zones(model.zone_weights(), world)
-    counts = [model.count(seed=123, z0=a, z1=b) for a, b in shards]
-    ph = model.emit(seed=123, z0=shards[rank][0], z1=shards[rank][1])
+    shards = G.zone_shards(model.zone_weights(), world)
+    counts = [model.count(seed=123, z0=a, z1=b, stride=st) for a, b, st in shards]
+    a, b, st = shards[rank]
+    ph = model.emit(seed=123, z0=a, z1=b, stride=st)
     orc = O.OracleModel(dump, photon_n=150 * world)
     orc.init(2)
     orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=123, id_base=int(sum(counts[:rank])), frozen=True,
@@ -82,7 +83,10 @@ def test_two_rank_shards_equal_single_job(dump32, tmp_path):
     spec_d = np.load(tmp_path / "spec.npy")
     ctr_d = np.load(tmp_path / "ctr.npy")
     model = G.Model.load(dump32, photon_n=150 * world).init(2)
-    ph = model.emit(seed=123)
+    # the ranks' photons in rank order: the ids they were tracked under
+    ph = np.concatenate([model.emit(seed=123, z0=a, z1=b, stride=st)
+                         for a, b, st in G.zone_shards(model.zone_weights(), world)])
+    assert len(ph) == model.count(seed=123)  # the shards' union is the single-GPU photon set
     orc = O.OracleModel(dump32, photon_n=150 * world)
     orc.init(2)
     orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=SNAP["scatt"],
@@ -119,14 +123,15 @@ def _stash_job(rank, world, dump, out_dir, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     model = G.Model.load(dump, photon_n=150 * world).init(2)
-    shards = G.shard_zones(model.zone_weights(), world)
+    shards = G.zone_shards(model.zone_weights(), world)
     k = len(STASH_SEEDS)
     st_spec = np.zeros((k, 15600))
     st_sum = np.zeros((k, 9), dtype=np.int64)
     st_max = np.zeros((k, 2), dtype=np.int64)
     for slot, seed in enumerate(STASH_SEEDS):
-        counts = [model.count(seed=seed, z0=a, z1=b) for a, b in shards]
-        ph = model.emit(seed=seed, z0=shards[rank][0], z1=shards[rank][1])
+        counts = [model.count(seed=seed, z0=a, z1=b, stride=st) for a, b, st in shards]
+        a, b, st = shards[rank]
+        ph = model.emit(seed=seed, z0=a, z1=b, stride=st)
         orc = O.OracleModel(dump, photon_n=150 * world)
         orc.init(2)
         orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=seed, id_base=int(sum(counts[:rank])), frozen=True,
@@ -157,7 +162,8 @@ def test_two_rank_stashed_passes_equal_single_jobs(dump32, tmp_path):
     st_max = np.load(tmp_path / "st_max.npy")
     model = G.Model.load(dump32, photon_n=150 * world).init(2)
     for slot, seed in enumerate(STASH_SEEDS):
-        ph = model.emit(seed=seed)
+        ph = np.concatenate([model.emit(seed=seed, z0=a, z1=b, stride=st)
+                             for a, b, st in G.zone_shards(model.zone_weights(), world)])
         orc = O.OracleModel(dump32, photon_n=150 * world)
         orc.init(2)
         orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=seed, id_base=0, frozen=True, scatt0=SNAP["scatt"],

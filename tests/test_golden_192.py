@@ -1,10 +1,12 @@
 """Headline-scale statistical fixtures (tests/golden/oracle_synth192_pn1e5.*, tools/make_golden_192.py):
-six oracle run_simulation runs (reference CPU semantics: serial, mt19937, live adaptive bias) on
+the oracle run_simulation runs (reference CPU semantics: serial, mt19937, live adaptive bias) on
 the 192x192 dump019-class synthetic dump at photon_n = 1e5 (BASELINE configs[0]).
 
 These tests calibrate the statistic the GPU parity test (tests/test_gpu_parity_192.py) applies to
 the device: independent reference-semantics runs must pass the binned Kish-N KS test on nu L_nu
-against each other, per theta bin and summed, at the test's own alpha."""
+against each other, per theta bin and summed, at the test's own alpha (1e-4 per statistic); at
+alpha = 1e-3 the fraction of the (pairs x 7) statistics over the threshold must stay near 1e-3 (a
+max over hundreds of pairs at 1e-3 would fail by chance)."""
 import json
 import os
 
@@ -19,14 +21,18 @@ G = os.path.join(HERE, "golden", "oracle_synth192_pn1e5")
 def test_oracle_seeds_pass_binned_ks():
     g = np.load(G + ".npz")
     cells = g["cells"]
-    worst = 0.0
+    worst, over, tot = 0.0, 0, 0
     for i in range(len(cells)):
         for j in range(i + 1, len(cells)):
             for th in [None, 0, 1, 2, 3, 4, 5]:
                 d, n1, n2 = binned_ks(cells[i], cells[j], th)
-                worst = max(worst, d / ks_crit(n1, n2, 1e-3))
-    print(f"worst D / crit(alpha=1e-3) over {len(cells) * (len(cells) - 1) // 2} seed pairs x 7: {worst:.2f}")
+                worst = max(worst, d / ks_crit(n1, n2, 1e-4))
+                over += d >= ks_crit(n1, n2, 1e-3)
+                tot += 1
+    print(f"{len(cells)} runs: worst D / crit(alpha=1e-4) over {tot} statistics: {worst:.2f}; over crit(1e-3): "
+          f"{over} of {tot}")
     assert worst < 1.0
+    assert over <= max(2, 0.01 * tot)
 
 
 def test_fixture_consistency():

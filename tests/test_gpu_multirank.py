@@ -2,19 +2,20 @@
 
 1. N-rank jobs emulated on one GPU (N = 2, 4, 8), live adaptive bias, against the oracle's
    run_simulation at the headline scale (192x192, photon_n = 1e5; tests/golden/oracle_synth192_pn1e5.*):
-   each emulated rank runs bench.py's contiguous zone shard as a pass of its own after a reset, so
-   its bias_func (harm_model.cpp:1391-1404) sees only its own counters, as on N GPUs; the ranks'
-   results are summed.  A shard of inner zones alone has a different scattering history than the
-   whole disk -- the question DESIGN.md §7 had left open -- so the job's counters are tested the way
-   the single-GPU job's are (tests/test_gpu_parity_192.py): the mean over N_DEV seeds against the
-   oracle's mean, and the KS test of one traced job.
+   each emulated rank runs bench.py's zone shard (grmonty_amd.zone_shards, strided: every N-th
+   zone) as a pass of its own after a reset, so its bias_func (harm_model.cpp:1391-1404) sees only
+   its own counters, as on N GPUs; the ranks' results are summed.  The job's counters are tested
+   the way the single-GPU job's are (tests/test_gpu_parity_192.py): the mean over N_DEV seeds
+   against the oracle's mean, and the KS test of one traced job.  (Contiguous zone ranges failed
+   this: +17 / +30 / +43 % recorded at 2 / 4 / 8 ranks, profiles/r03a_multirank_contiguous.log.)
 
 2. The multi-rank reduction on the engine's own stash buffers: two processes on the GPU, one engine
    each, run the two shards of a frozen-bias job (so the result is exact), stash their passes
    (grm_engine_stash: the engine's packing), read the raw slots (grm_engine_stash_raw), reduce them
    over gloo -- the spectrum and the "sum" words summed, the "max" words maxed, which is what
    grm_engine_allreduce_stash asks RCCL for -- write them back and decode them with
-   grm_engine_stash_read.  Must equal one engine tracking the whole job: this checks the stash
+   grm_engine_stash_read.  Must equal one engine tracking the ranks' photons concatenated (the
+   same photon ids): this checks the stash
    word order, the split of the counters between sum and max and the slot indexing, which RCCL
    with N > 1 would reduce the same way (RCCL itself with N > 1 needs N GPUs: not run here).
 """
@@ -51,7 +52,7 @@ def setup192(dump_dir):
 def test_emulated_ranks_vs_oracle(setup192, world):
     import grmonty_amd as GA
     model, eng = setup192
-    shards = GA.shard_zones(model.zone_weights(), world)
+    shards = GA.zone_shards(model.zone_weights(), world)
     summ = json.load(open(GOLD + ".json"))
     o = {k: np.array([r[k] for r in summ["runs"]], dtype=np.float64) for k in KEYS}
     dev = {k: [] for k in KEYS}
@@ -114,14 +115,15 @@ def _rank(rank, world, dump, out_dir, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     model = G.Model.load(dump, photon_n=3000).init(4)
-    shards = G.shard_zones(model.zone_weights(), world)
+    shards = G.zone_shards(model.zone_weights(), world)
     eng = G.Engine(model, device=0)
     eng.emit_setup(model)
     eng.stash_reserve(len(SEEDS))
     for slot, seed in enumerate(SEEDS):
-        base = sum(model.count(seed=seed, z0=a, z1=b) for a, b in shards[:rank])
+        base = sum(model.count(seed=seed, z0=a, z1=b, stride=st) for a, b, st in shards[:rank])
         _configure(G, eng, model, seed, base)
-        p, n = eng.emit(seed=seed, z0=shards[rank][0], z1=shards[rank][1])
+        a, b, st = shards[rank]
+        p, n = eng.emit(seed=seed, z0=a, z1=b, stride=st)
         eng.track_device(p, n)
         eng.stash(slot)
     spec, sums, maxs = eng.stash_raw(len(SEEDS))
@@ -154,12 +156,13 @@ def test_gloo_reduction_of_engine_stash(dump64, tmp_path):
     mt_d = np.load(tmp_path / "maxtau.npy")
     raw = np.load(tmp_path / "raw_sums.npy")
     model = G.Model.load(dump64, photon_n=3000).init(4)
+    shards = G.zone_shards(model.zone_weights(), world)
     eng = G.Engine(model, device=0)
-    eng.emit_setup(model)
     for slot, seed in enumerate(SEEDS):
         _configure(G, eng, model, seed, 0)
-        p, n = eng.emit(seed=seed)
-        eng.track_device(p, n)
+        ph = np.concatenate([model.emit(seed=seed, z0=a, z1=b, stride=st) for a, b, st in shards])
+        n = len(ph)
+        eng.track(ph)
         spec1, nr, ns, mt = eng.finish()
         st = eng.stats()
         print(f"seed {seed}: one engine recorded {nr} scattered {ns} steps {st['n_steps']}; two ranks "

@@ -75,7 +75,8 @@ def test_watchdog_abandons_and_recovers(model64):
 
 def test_kernel_argument_guard(model64):
     import grmonty_amd as G
-    ph = model64.emit(seed=123)[:3000]
+    full = model64.emit(seed=123)
+    ph = full[np.random.default_rng(5).permutation(len(full))[:3000]]  # all radii (zone order starts inside)
     eng = G.Engine(model64, device=0)
     _frozen(G, eng)
     eng.track(ph)

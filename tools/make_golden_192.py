@@ -82,7 +82,7 @@ def main():
     res = old + res
     res.sort(key=lambda r: r["seed"])
     spec = next(r["spectrum"] for r in res if r["spectrum"] is not None)
-    np.savez_compressed(OUT + ".npz", seeds=np.array(seeds), cells=np.stack([r["cells"] for r in res]),
+    np.savez_compressed(OUT + ".npz", seeds=np.array([r["seed"] for r in res]), cells=np.stack([r["cells"] for r in res]),
                         spectrum123=spec,
                         counters=np.array([[r["counters"][k] for k in ("created", "scattered", "recorded", "steps")]
                                            for r in res], dtype=np.int64),
