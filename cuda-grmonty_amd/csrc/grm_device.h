@@ -333,7 +333,16 @@ struct Conn {
     double c[4][10]; /* [i][tri(j,k)], tri: 00 01 02 03 11 12 13 22 23 33 */
 };
 
-__device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn &C) {
+/* the products the 40 entries share (computed once per point) */
+struct ConnPre {
+    double r1, r2, r3, r4, a, a2, a3, a4;
+    double sth, cth, sth2, r1sth2, sth4, cth2, cth4, s2th, c2th, a2sth2, a2cth2, a4cth4;
+    double dthdx2, d2thdx22, rho2, rho22, rho23, irho2, irho22, irho23, idthdx2, irho23_dthdx2;
+    double fac1, fac1_rho23, fac3, i_r1rho23, i_sth;
+    double r1f, a2s2d, r1s2d, d2r, fac3f, arcd;
+};
+
+__device__ __forceinline__ void connection_pre(const Params &P, const Trig &T, ConnPre &Q) {
     const double r1 = T.r1, r2 = r1 * r1, r3 = r2 * r1, r4 = r3 * r1;
     const double hs = P.h_slope;
     const double dthdx2 = kPi * (1.0 + (1.0 - hs) * T.c2x);
@@ -353,66 +362,92 @@ __device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn 
     const double i_r1rho23 = frcp(r1) * irho23;
     /* the reference's fac2 = a^2 + 2 r^2 + a^2 cos(2 theta) = 2 rho^2: written through rho^2 below */
     const double i_sth = frcp(sth);
-
+    Q.r1 = r1; Q.r2 = r2; Q.r3 = r3; Q.r4 = r4;
+    Q.a = a; Q.a2 = a2; Q.a3 = a3; Q.a4 = a4;
+    Q.sth = sth; Q.cth = cth; Q.sth2 = sth2; Q.r1sth2 = r1sth2; Q.sth4 = sth4; Q.cth2 = cth2; Q.cth4 = cth4;
+    Q.s2th = s2th; Q.c2th = c2th; Q.a2sth2 = a2sth2; Q.a2cth2 = a2cth2; Q.a4cth4 = a4cth4;
+    Q.dthdx2 = dthdx2; Q.d2thdx22 = d2thdx22; Q.rho2 = rho2; Q.rho22 = rho22; Q.rho23 = rho23;
+    Q.irho2 = irho2; Q.irho22 = irho22; Q.irho23 = irho23; Q.idthdx2 = idthdx2; Q.irho23_dthdx2 = irho23_dthdx2;
+    Q.fac1 = fac1; Q.fac1_rho23 = fac1_rho23; Q.fac3 = fac3; Q.i_r1rho23 = i_r1rho23; Q.i_sth = i_sth;
     /* products shared between entries (reassociated: agreement with the reference's expressions to a
      * few ulp, tests/test_gpu_probes.py::test_connection) */
-    const double r1f = r1 * fac1_rho23;                      /* r fac1 / rho^6 */
-    const double a2s2d = a2 * s2th * dthdx2 * irho22;         /* a^2 sin 2th dth/dx2 / rho^4 */
-    const double r1s2d = r1 * s2th * irho23_dthdx2;           /* r sin 2th / (rho^6 dth/dx2) */
-    const double d2r = dthdx22 * irho2;                       /* (dth/dx2)^2 / rho^2 */
-    const double fac3f = fac3 * fac1 * i_r1rho23;
-    const double arcd = a * r1 * cth * dthdx2 * i_sth * irho22;
+    Q.r1f = r1 * fac1_rho23;                      /* r fac1 / rho^6 */
+    Q.a2s2d = a2 * s2th * dthdx2 * irho22;         /* a^2 sin 2th dth/dx2 / rho^4 */
+    Q.r1s2d = r1 * s2th * irho23_dthdx2;           /* r sin 2th / (rho^6 dth/dx2) */
+    Q.d2r = dthdx22 * irho2;                       /* (dth/dx2)^2 / rho^2 */
+    Q.fac3f = fac3 * fac1 * i_r1rho23;
+    Q.arcd = a * r1 * cth * dthdx2 * i_sth * irho22;
+}
 
-    C.c[0][0] = 2.0 * r1f;
-    C.c[0][1] = (2.0 * r1 + rho2) * r1f;
-    C.c[0][2] = -r1 * a2s2d;
-    C.c[0][3] = -2.0 * a * sth2 * r1f;
-    C.c[0][4] = 2.0 * r2 * (r4 + r1 * fac1 - a4cth4) * irho23;
-    C.c[0][5] = -r2 * a2s2d;
-    C.c[0][6] = a * r1 * (-r1 * (r3 + 2.0 * fac1) + a4cth4) * sth2 * irho23;
-    C.c[0][7] = -2.0 * r2 * d2r;
-    C.c[0][8] = a * r1sth2 * a2s2d;
-    C.c[0][9] = 2.0 * r1sth2 * (-r1 * rho22 + a2sth2 * fac1) * irho23;
+/* row i of the connection, Gamma^i_{jk} for j <= k in tri order (harm_model.cpp:1436-1569) */
+__device__ __forceinline__ void connection_row(const ConnPre &Q, int i, double L[10]) {
+    const double r1 = Q.r1, r2 = Q.r2, r3 = Q.r3, r4 = Q.r4, a = Q.a, a2 = Q.a2, a3 = Q.a3, a4 = Q.a4;
+    const double sth = Q.sth, cth = Q.cth, sth2 = Q.sth2, r1sth2 = Q.r1sth2, sth4 = Q.sth4, cth2 = Q.cth2,
+                 cth4 = Q.cth4;
+    const double s2th = Q.s2th, c2th = Q.c2th, a2sth2 = Q.a2sth2, a2cth2 = Q.a2cth2, a4cth4 = Q.a4cth4;
+    const double dthdx2 = Q.dthdx2, d2thdx22 = Q.d2thdx22, rho2 = Q.rho2, rho22 = Q.rho22, rho23 = Q.rho23;
+    const double irho2 = Q.irho2, irho22 = Q.irho22, irho23 = Q.irho23, idthdx2 = Q.idthdx2,
+                 irho23_dthdx2 = Q.irho23_dthdx2;
+    const double fac1 = Q.fac1, fac1_rho23 = Q.fac1_rho23, fac3 = Q.fac3, i_r1rho23 = Q.i_r1rho23, i_sth = Q.i_sth;
+    const double r1f = Q.r1f, a2s2d = Q.a2s2d, r1s2d = Q.r1s2d, d2r = Q.d2r, fac3f = Q.fac3f, arcd = Q.arcd;
+    if (i == 0) {
+        L[0] = 2.0 * r1f;
+        L[1] = (2.0 * r1 + rho2) * r1f;
+        L[2] = -r1 * a2s2d;
+        L[3] = -2.0 * a * sth2 * r1f;
+        L[4] = 2.0 * r2 * (r4 + r1 * fac1 - a4cth4) * irho23;
+        L[5] = -r2 * a2s2d;
+        L[6] = a * r1 * (-r1 * (r3 + 2.0 * fac1) + a4cth4) * sth2 * irho23;
+        L[7] = -2.0 * r2 * d2r;
+        L[8] = a * r1sth2 * a2s2d;
+        L[9] = 2.0 * r1sth2 * (-r1 * rho22 + a2sth2 * fac1) * irho23;
+    } else if (i == 1) {
+        L[0] = fac3f;
+        L[1] = fac1 * (-2.0 * r1 + a2sth2) * irho23;
+        L[2] = 0.0;
+        L[3] = -a * sth2 * fac3f;
+        L[4] = (r4 * (-2.0 + r1) * (1.0 + r1) +
+                a2 * (a2 * r1 * (1.0 + 3.0 * r1) * cth4 + a4cth4 * cth2 + r3 * sth2 +
+                      r1 * cth2 * (2.0 * r1 + 3.0 * r3 - a2sth2))) *
+               irho23;
+        L[5] = -0.5 * rho2 * a2s2d; /* -a^2 dth/dx2 sin 2th / (2 rho^2) */
+        L[6] = a * sth2 * (a4 * r1 * cth4 + r2 * (2.0 * r1 + r3 - a2sth2) + a2cth2 * (2.0 * r1 * (-1.0 + r2) + a2sth2)) *
+               irho23;
+        L[7] = -fac3 * d2r;
+        L[8] = 0.0;
+        L[9] = -fac3 * sth2 * (r1 * rho22 - a2 * fac1 * sth2) * i_r1rho23;
+    } else if (i == 2) {
+        L[0] = -a2 * r1s2d;
+        L[1] = r1 * L[0];
+        L[2] = 0.0;
+        L[3] = a * (a2 + r2) * r1s2d;
+        L[4] = r2 * L[0];
+        L[5] = r2 * irho2;
+        L[6] = (a * r1 * cth * sth * (r3 * (2.0 + r1) + a2 * (2.0 * r1 * (1.0 + r1) * cth2 + a2 * cth4 + 2.0 * r1sth2))) *
+               irho23_dthdx2;
+        L[7] = -a2 * cth * sth * dthdx2 * irho2 + d2thdx22 * idthdx2;
+        L[8] = 0.0;
+        L[9] = -cth * sth * (rho23 + a2sth2 * rho2 * (r1 * (4.0 + r1) + a2cth2) + 2.0 * r1 * a4 * sth4) * irho23_dthdx2;
+    } else {
+        L[0] = a * fac1_rho23;
+        L[1] = a * r1f;
+        L[2] = -2.0 * arcd;
+        L[3] = -a2sth2 * fac1_rho23;
+        L[4] = a * r1 * r1f;
+        /* ifac2^2 = irho2^2 / 4 */
+        L[5] = -0.5 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * arcd;
+        L[6] = r1 * (r1 * rho22 - a2sth2 * fac1) * irho23;
+        L[7] = -a * r1 * d2r;
+        L[8] = dthdx2 * (rho22 * cth * i_sth + a2 * r1 * s2th) * irho22; /* fac2^2 / 4 = rho^4 */
+        L[9] = (-a * r1sth2 * rho22 + a3 * sth4 * fac1) * irho23;
+    }
+}
 
-    C.c[1][0] = fac3f;
-    C.c[1][1] = fac1 * (-2.0 * r1 + a2sth2) * irho23;
-    C.c[1][2] = 0.0;
-    C.c[1][3] = -a * sth2 * fac3f;
-    C.c[1][4] = (r4 * (-2.0 + r1) * (1.0 + r1) +
-                 a2 * (a2 * r1 * (1.0 + 3.0 * r1) * cth4 + a4cth4 * cth2 + r3 * sth2 +
-                       r1 * cth2 * (2.0 * r1 + 3.0 * r3 - a2sth2))) *
-                irho23;
-    C.c[1][5] = -0.5 * rho2 * a2s2d; /* -a^2 dth/dx2 sin 2th / (2 rho^2) */
-    C.c[1][6] = a * sth2 * (a4 * r1 * cth4 + r2 * (2.0 * r1 + r3 - a2sth2) + a2cth2 * (2.0 * r1 * (-1.0 + r2) + a2sth2)) *
-                irho23;
-    C.c[1][7] = -fac3 * d2r;
-    C.c[1][8] = 0.0;
-    C.c[1][9] = -fac3 * sth2 * (r1 * rho22 - a2 * fac1 * sth2) * i_r1rho23;
-
-    C.c[2][0] = -a2 * r1s2d;
-    C.c[2][1] = r1 * C.c[2][0];
-    C.c[2][2] = 0.0;
-    C.c[2][3] = a * (a2 + r2) * r1s2d;
-    C.c[2][4] = r2 * C.c[2][0];
-    C.c[2][5] = r2 * irho2;
-    C.c[2][6] = (a * r1 * cth * sth * (r3 * (2.0 + r1) + a2 * (2.0 * r1 * (1.0 + r1) * cth2 + a2 * cth4 + 2.0 * r1sth2))) *
-                irho23_dthdx2;
-    C.c[2][7] = -a2 * cth * sth * dthdx2 * irho2 + d2thdx22 * idthdx2;
-    C.c[2][8] = 0.0;
-    C.c[2][9] = -cth * sth * (rho23 + a2sth2 * rho2 * (r1 * (4.0 + r1) + a2cth2) + 2.0 * r1 * a4 * sth4) *
-                irho23_dthdx2;
-
-    C.c[3][0] = a * fac1_rho23;
-    C.c[3][1] = a * r1f;
-    C.c[3][2] = -2.0 * arcd;
-    C.c[3][3] = -a2sth2 * fac1_rho23;
-    C.c[3][4] = a * r1 * r1f;
-    /* ifac2^2 = irho2^2 / 4 */
-    C.c[3][5] = -0.5 * (a2 + 2.0 * r1 * (2.0 + r1) + a2 * c2th) * arcd;
-    C.c[3][6] = r1 * (r1 * rho22 - a2sth2 * fac1) * irho23;
-    C.c[3][7] = -a * r1 * d2r;
-    C.c[3][8] = dthdx2 * (rho22 * cth * i_sth + a2 * r1 * s2th) * irho22; /* fac2^2 / 4 = rho^4 */
-    C.c[3][9] = (-a * r1sth2 * rho22 + a3 * sth4 * fac1) * irho23;
+__device__ __forceinline__ void connection(const Params &P, const Trig &T, Conn &C) {
+    ConnPre Q;
+    connection_pre(P, T, Q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) connection_row(Q, i, C.c[i]);
 }
 
 /* dk^i/dlambda = -Gamma^i_{jk} k^j k^k (harm_model.cpp:1255-1262, 1578-1586) */
@@ -496,6 +531,54 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
     connection(P, T, C);
     gcov_from_trig(P, T, G);
     return push_finish(C, k, kp, dk, dl, e_0_s, G.g00, G.g01, G.g03, e_1);
+}
+
+/* push_attempt for a wave whose lanes all hold the same push state (the lone pipeline's geometry
+ * wave): the same operations and roundings, with the connection contracted over the lanes.  Lane l
+ * forms row l & 3 of the connection only (four divergent blocks: the connection's instructions are
+ * issued once, as in push_attempt) and contracts it with kc -- geo_rhs's expression -- so one
+ * contraction per corrector pass instead of four; lanes 0..3 hand dk^0..3 to every lane by
+ * v_readlane.  Bit-identical to push_attempt. */
+__device__ __forceinline__ double rows_bcast(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, src), hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ bool push_attempt_rows(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
+                                                  double dl, double &e_1, int lane) {
+    double kp[4];
+    push_kick(x, k, dk, dl, kp);
+    Trig T;
+    trig_at(P, x, T);
+    ConnPre Q;
+    connection_pre(P, T, Q);
+    double L[10];
+    connection_row(Q, lane & 3, L);
+    Gcov G;
+    gcov_from_trig(P, T, G);
+    const double dl_2 = 0.5 * dl;
+    double err;
+    int iter = 0;
+    do {
+        ++iter;
+        const double kc[4] = {kp[0], kp[1], kp[2], kp[3]};
+        /* geo_rhs (same expression) with this lane's row */
+        double d = -2.0 * (kc[0] * (L[1] * kc[1] + L[2] * kc[2] + L[3] * kc[3]) + kc[1] * (L[5] * kc[2] + L[6] * kc[3]) +
+                           L[8] * kc[2] * kc[3]);
+        d -= (L[0] * kc[0] * kc[0] + L[4] * kc[1] * kc[1] + L[7] * kc[2] * kc[2] + L[9] * kc[3] * kc[3]);
+        err = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            dk[i] = rows_bcast(d, i);
+            kp[i] = k[i] + dl_2 * dk[i];
+            err += fratio_tol(kc[i] - kp[i], kp[i] + EPS);
+        }
+    } while (err > E_TOL && iter < MAX_ITER);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k[i] = kp[i];
+    e_1 = -(k[0] * G.g00 + k[1] * G.g01 + k[3] * G.g03);
+    const bool err_e = fabs(e_1 - e_0_s) > 1.0e-4 * fabs(e_0_s);
+    return (err_e || err > E_TOL || isnan(err) || isinf(err));
 }
 
 /* Per-lane spill slot for the push backup, laid out [component][lane] so that a wave's

@@ -43,12 +43,12 @@ def cell_sums(tr):
 
 
 def run(args):
-    path, photon_n, seed = args
+    path, photon_n, seed, cap = args
     import oracle_py as O
     m = O.OracleModel(path, photon_n=photon_n)
     m.init(1)
-    t, tr, n_tr = m.run_simulation_traced(seed=seed, trace_cap=1 << 24)
-    assert n_tr <= (1 << 24), "trace overflow"
+    t, tr, n_tr = m.run_simulation_traced(seed=seed, trace_cap=cap)
+    assert n_tr <= cap, "trace overflow"
     c = m.counters()
     rep = m.report(None)
     return dict(seed=seed, wall_s=t, counters=c, luminosity=rep["luminosity"], max_tau_scatt=rep["max_tau_scatt"],
@@ -61,14 +61,18 @@ def main():
     ap.add_argument("--photon-n", type=float, default=1e5)
     ap.add_argument("--grid", type=int, default=192)
     ap.add_argument("--merge", action="store_true", help="append to the committed fixtures")
+    ap.add_argument("--out", default=OUT, help="fixture path prefix (.npz / .json)")
+    ap.add_argument("--trace-cap", type=int, default=1 << 24, help="photon ends traced per run")
+    ap.add_argument("--procs", type=int, default=0, help="parallel runs (default: one per seed)")
     args = ap.parse_args()
+    out = args.out
     from grmonty_amd.synth_dump import ensure_dump
     path = ensure_dump(os.path.join("/tmp", f"synth{args.grid}.dump"), args.grid, args.grid)
     seeds = [int(s) for s in args.seeds.split(",")]
     old = []
     if args.merge:
-        g = np.load(OUT + ".npz")
-        js = json.load(open(OUT + ".json"))
+        g = np.load(out + ".npz")
+        js = json.load(open(out + ".json"))
         for i, r in enumerate(js["runs"]):
             old.append(dict(seed=r["seed"], wall_s=r["wall_s"], luminosity=r["luminosity"],
                             max_tau_scatt=r["max_tau_scatt"], cells=g["cells"][i],
@@ -76,13 +80,13 @@ def main():
                             spectrum=g["spectrum123"] if r["seed"] == 123 else None))
         seeds = [s for s in seeds if s not in {r["seed"] for r in old}]
     t = time.time()
-    with mp.Pool(max(1, len(seeds))) as pool:
-        res = pool.map(run, [(path, int(args.photon_n), s) for s in seeds])
+    with mp.Pool(args.procs or max(1, len(seeds))) as pool:
+        res = pool.map(run, [(path, int(args.photon_n), s, args.trace_cap) for s in seeds])
     print(f"{len(seeds)} oracle runs in {time.time() - t:.0f} s")
     res = old + res
     res.sort(key=lambda r: r["seed"])
     spec = next(r["spectrum"] for r in res if r["spectrum"] is not None)
-    np.savez_compressed(OUT + ".npz", seeds=np.array([r["seed"] for r in res]), cells=np.stack([r["cells"] for r in res]),
+    np.savez_compressed(out + ".npz", seeds=np.array([r["seed"] for r in res]), cells=np.stack([r["cells"] for r in res]),
                         spectrum123=spec,
                         counters=np.array([[r["counters"][k] for k in ("created", "scattered", "recorded", "steps")]
                                            for r in res], dtype=np.int64),
@@ -96,7 +100,7 @@ def main():
         v = np.array([x[key] for x in summ["runs"]], dtype=np.float64)
         summ.setdefault("mean", {})[key] = float(v.mean())
         summ.setdefault("std", {})[key] = float(v.std(ddof=1))
-    with open(OUT + ".json", "w") as fh:
+    with open(out + ".json", "w") as fh:
         json.dump(summ, fh, indent=1)
     print(json.dumps(summ, indent=1))
 
