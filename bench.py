@@ -221,11 +221,34 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         engine.comm_init(uid[0], world, rank)
     engine.emit_setup(model)  # the zone table is resident in HBM before the timed region
+    bias_counters = "single GPU"
+    if world > 1:
+        # pass slots: warm-up passes 0..W-1, timed passes W..W+K-1 (each pass its own counter block)
+        engine.stash_reserve(len(warm_seeds) + len(timed_seeds))
+        # the job's adaptive bias: every rank's kernels read every rank's counter block of the pass
+        # (IPC over xGMI, grm_engine_set_peers); without it each rank's bias would run on a history N
+        # times shorter
+        handles = [None] * world
+        dist.all_gather_object(handles, engine.counters_ipc_handle())
+        ok = True
+        try:
+            engine.set_peers(handles, rank)
+        except RuntimeError as ex:
+            ok = False
+            print(f"rank {rank}: peer counters unavailable ({ex}); per-rank bias counters", file=sys.stderr)
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        if not all(flags):
+            engine.set_peers([], rank)
+        bias_counters = "job-wide (peer counter blocks over xGMI)" if all(flags) else "per rank (IPC unavailable)"
 
     def one_pass(eng, seed, base, slot):
         """one run_simulation pass on this rank's shard: emission + transport + readback; with
         several ranks its results are stashed on the device (slot) for the job's one all-reduce"""
-        eng.reset()
+        if slot is None:
+            eng.reset()
+        else:
+            eng.begin_pass(slot)
         eng.set_option(G.OPT_SEED, seed)
         eng.set_option(G.OPT_ID_BASE, base)
         ptr, n_dev = eng.emit(seed=seed, z0=z0, z1=z1, stride=zst)
@@ -238,19 +261,17 @@ def main():
             raise RuntimeError(f"pass seed {seed}: {st['n_dropped']} children dropped, {st['n_abandoned']} abandoned")
         return n_dev, st, n_rec, n_scatt
 
-    def reduce_job(eng, n):
+    def reduce_job(eng, first, n):
         """the job's one exchange: a grouped RCCL all-reduce of every pass's stashed results, then
         each pass's reduced spectrum and counters read back (the ranks' pass timelines stay
         uncoupled: a rank held up by a long-lived photon does not stall the others pass by pass)"""
-        eng.allreduce_stash(n)
-        return [eng.stash_read(s) for s in range(n)]
+        eng.allreduce_stash(first + n)
+        return [eng.stash_read(first + s) for s in range(n)]
 
-    if world > 1:
-        engine.stash_reserve(max(len(warm_seeds), len(timed_seeds)))
     for i, sd in enumerate(warm_seeds):
         one_pass(engine, sd, id_base[sd], i if world > 1 else None)
     if world > 1 and warm_seeds:
-        reduce_job(engine, len(warm_seeds))
+        reduce_job(engine, 0, len(warm_seeds))
     launches0 = engine.stats()["n_launches"]
     if dist is not None:
         dist.barrier()
@@ -258,9 +279,9 @@ def main():
     t0 = time.time()
     for i, sd in enumerate(timed_seeds):
         tp = time.time()
-        res.append(one_pass(engine, sd, id_base[sd], i if world > 1 else None))
+        res.append(one_pass(engine, sd, id_base[sd], len(warm_seeds) + i if world > 1 else None))
         pass_s.append(time.time() - tp)
-    job = reduce_job(engine, len(timed_seeds)) if world > 1 else None
+    job = reduce_job(engine, len(warm_seeds), len(timed_seeds)) if world > 1 else None
     if dist is not None:
         dist.barrier()
     elapsed = time.time() - t0
@@ -339,6 +360,7 @@ def main():
                                    f"mass_unit=4e19, zone-sharded over {world} GPU(s)",
                        "photon_n_job": photon_n_job, "grid": f"{args.grid}x{args.grid}",
                        "superphotons_per_pass_rank0": n_rank // max(1, args.steps),
+                       "bias_counters": bias_counters,
                        "parallelism": f"strided zone shards x{world}" + (", passes stashed on the device, one RCCL all-reduce per job"
                                                                   if world > 1 else "")},
             "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",

@@ -143,6 +143,12 @@ struct Ctl {
     unsigned long long *early_tail, *early_head, *early_done, *wg_exit, *early_live, *bulk_live;
     int early_steps;
     int karg_test; /* test only (GRM_OPT_KARG_TEST): the kernel-argument check expects lanes + this */
+    /* The job's bias counters across ranks: peers[r] = rank r's array of per-pass counter blocks
+     * (its own included; remote ones mapped over xGMI by IPC), ctr_slot = this pass's block.  With
+     * n_peers > 1 bias_func's running counters are the whole job's: the sums of n_scatt and
+     * n_recorded and the max of max tau_scatt over the ranks' blocks of this pass. */
+    const DevCounters *const *peers;
+    int n_peers, ctr_slot;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -203,6 +209,26 @@ __device__ __forceinline__ double bias_den(const Params &P, const Ctl &C) {
         scatt = C.f_scatt;
         rec = C.f_rec;
         mts = C.f_maxtau;
+    } else if (C.n_peers > 1) {
+        /* the job's counters: lane r reads rank r's block of this pass (one remote round trip for
+         * the wave, every REFRESH_TRIPS trips), then a wave reduction (converged callers only) */
+        const int lane = (int)(threadIdx.x & 63);
+        unsigned long long sc = 0, rc = 0, mt = 0;
+        if (lane < C.n_peers) {
+            const DevCounters *pc = C.peers[lane] + C.ctr_slot;
+            sc = __hip_atomic_load(&pc->n_scatt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            rc = __hip_atomic_load(&pc->n_recorded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            mt = __hip_atomic_load(&pc->max_tau_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            sc += __shfl_xor(sc, o);
+            rc += __shfl_xor(rc, o);
+            mt = max(mt, (unsigned long long)__shfl_xor(mt, o));
+        }
+        scatt = (double)sc;
+        rec = (double)rc;
+        mts = __longlong_as_double((long long)mt);
     } else { /* live, reference-like adaptive bias */
         scatt = (double)__hip_atomic_load(&C.ctr->n_scatt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rec = (double)__hip_atomic_load(&C.ctr->n_recorded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2035,8 +2061,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
 #ifdef GRM_TIMING
     if (lane_id == 0) {
         g_tlds[threadIdx.x >> 6][3] = __builtin_amdgcn_s_memtime() - t_start;
-        for (int r = 0; r < 15; ++r) atomicAdd(C.timing + r, g_tlds[threadIdx.x >> 6][r]);
-        for (int r = 16; r < 24; ++r) atomicAdd(C.timing + 16 + r, g_tlds[threadIdx.x >> 6][r]);
+        for (int r = 0; r < 15; ++r) atomicAdd(C0.timing + r, g_tlds[threadIdx.x >> 6][r]);
+        for (int r = 16; r < 24; ++r) atomicAdd(C0.timing + 16 + r, g_tlds[threadIdx.x >> 6][r]);
     }
 #endif
     const Ctl &C = C0;
@@ -2133,6 +2159,31 @@ __global__ __launch_bounds__(256) void stash_kernel(const double *spec, const De
     }
 }
 
+/* the job's bias counters as bias_den forms them (grm_engine_job_counters; tests of the peer mapping) */
+__global__ __launch_bounds__(64) void job_counters_kernel(Params P, Ctl C, double *out) {
+    const double den = bias_den(P, C);
+    unsigned long long sc = 0, rc = 0, mt = 0;
+    const int lane = (int)threadIdx.x;
+    if (lane < C.n_peers) {
+        const DevCounters *pc = C.peers[lane] + C.ctr_slot;
+        sc = __hip_atomic_load(&pc->n_scatt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        rc = __hip_atomic_load(&pc->n_recorded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        mt = __hip_atomic_load(&pc->max_tau_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sc += __shfl_xor(sc, o);
+        rc += __shfl_xor(rc, o);
+        mt = max(mt, (unsigned long long)__shfl_xor(mt, o));
+    }
+    if (lane == 0) {
+        out[0] = den;
+        out[1] = (double)sc;
+        out[2] = (double)rc;
+        out[3] = __longlong_as_double((long long)mt);
+    }
+}
+
 __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
     if (op.reset)
         for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < op.n_spec; i += (size_t)gridDim.x * 256)
@@ -2166,7 +2217,13 @@ struct grm_engine {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     Params P{};
     double *d_zones = nullptr, *d_hot = nullptr, *d_k2 = nullptr;
-    DevCounters *d_ctr = nullptr;
+    DevCounters *d_ctr = nullptr;       /* the counter block in use: d_ctr_own, or a pass slot */
+    DevCounters *d_ctr_own = nullptr;   /* allocated with the engine */
+    DevCounters *d_ctr_slots = nullptr; /* per-pass blocks (grm_engine_stash_reserve), shared with peers */
+    int n_ctr_slots = 0, ctr_slot = -1;
+    const DevCounters **d_peers = nullptr; /* device array: every rank's d_ctr_slots */
+    int n_peers = 0;
+    std::vector<void *> ipc_open;           /* peers' blocks opened by IPC (closed at destroy) */
     grm_spectrum_cell *d_spec = nullptr;
     SReq *d_stack = nullptr;
     Cold *d_cold = nullptr;
@@ -2354,6 +2411,9 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.spec = e->d_spec;
     C.spec_blocks = e->d_spec_blocks;
     C.ctr = e->d_ctr;
+    C.peers = e->d_peers;
+    C.n_peers = (e->ctr_slot >= 0 && e->d_peers) ? e->n_peers : 0;
+    C.ctr_slot = e->ctr_slot;
     C.trace = e->trace_cap ? e->d_trace : nullptr;
     C.trace_cap = e->trace_cap;
     C.trace_count = e->d_small + 3;
@@ -2639,7 +2699,7 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     if (!hip_ok(e, hipMalloc(&e->d_zones, nz * 8 * sizeof(double)), "zones") ||
         !hip_ok(e, hipMalloc(&e->d_hot, nhot * sizeof(double)), "hotcross") ||
         !hip_ok(e, hipMalloc(&e->d_k2, (GRM_N_E_SAMP + 1) * sizeof(double)), "k2") ||
-        !hip_ok(e, hipMalloc(&e->d_ctr, sizeof(DevCounters)), "counters") ||
+        !hip_ok(e, hipMalloc(&e->d_ctr_own, sizeof(DevCounters)), "counters") ||
         !hip_ok(e, hipMalloc(&e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS), "spectrum") ||
         !hip_ok(e, hipMalloc(&e->d_small, 16 * sizeof(unsigned long long)), "small") ||
         !hip_ok(e, hipMalloc(&e->d_stuck, STUCK_CAP * STUCK_WORDS * sizeof(double)), "stuck") ||
@@ -2686,6 +2746,7 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     P.zones = e->d_zones;
     P.hotcross = e->d_hot;
     P.k2 = e->d_k2;
+    e->d_ctr = e->d_ctr_own;
     if (!hip_ok(e, hipMalloc(&e->d_timing, 48 * sizeof(unsigned long long)), "timing") ||
         !hip_ok(e, hipMemset(e->d_timing, 0, 48 * sizeof(unsigned long long)), "timing"))
         return fail();
@@ -2702,7 +2763,10 @@ void grm_engine_destroy(grm_engine *e) {
     hipFree(e->d_zones);
     hipFree(e->d_hot);
     hipFree(e->d_k2);
-    hipFree(e->d_ctr);
+    hipFree(e->d_ctr_own);
+    for (void *p : e->ipc_open) hipIpcCloseMemHandle(p);
+    hipFree(e->d_ctr_slots);
+    hipFree(e->d_peers);
     hipFree(e->d_spec);
     hipFree(e->d_stack);
     hipFree(e->d_cold);
@@ -3054,7 +3118,133 @@ int grm_engine_stash_reserve(grm_engine *e, int n_slots) {
     HIPCHK(e, hipMalloc(&e->d_stash_sum, (size_t)n_slots * STASH_SUMS * sizeof(unsigned long long)));
     HIPCHK(e, hipMalloc(&e->d_stash_max, (size_t)n_slots * STASH_MAXS * sizeof(unsigned long long)));
     e->stash_cap = n_slots;
+    /* per-pass counter blocks (grm_engine_begin_pass); a new allocation unlinks the peers */
+    if (e->ctr_slot >= 0) e->d_ctr = e->d_ctr_own;
+    e->ctr_slot = -1;
+    hipFree(e->d_ctr_slots);
+    e->d_ctr_slots = nullptr;
+    e->n_ctr_slots = 0;
+    hipFree(e->d_peers);
+    e->d_peers = nullptr;
+    e->n_peers = 0;
+    HIPCHK(e, hipMalloc(&e->d_ctr_slots, (size_t)n_slots * sizeof(DevCounters)));
+    HIPCHK(e, hipMemset(e->d_ctr_slots, 0, (size_t)n_slots * sizeof(DevCounters)));
+    e->n_ctr_slots = n_slots;
     return 0;
+}
+
+int grm_engine_begin_pass(grm_engine *e, int slot) {
+    if (!e) return -1;
+    if (slot >= e->n_ctr_slots) {
+        e->err = "grm_engine_begin_pass: slot " + std::to_string(slot) + " outside the reserved " +
+                 std::to_string(e->n_ctr_slots) + " (grm_engine_stash_reserve)";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->ctr_slot = slot < 0 ? -1 : slot;
+    e->d_ctr = slot < 0 ? e->d_ctr_own : e->d_ctr_slots + slot;
+    return grm_engine_reset(e);
+}
+
+int grm_engine_counters_ipc_handle(grm_engine *e, uint8_t out[64]) {
+    if (!e || !out) return -1;
+    if (!e->d_ctr_slots) {
+        e->err = "grm_engine_counters_ipc_handle: no pass slots (grm_engine_stash_reserve first)";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    hipIpcMemHandle_t h;
+    HIPCHK(e, hipIpcGetMemHandle(&h, e->d_ctr_slots));
+    static_assert(sizeof(h) <= 64, "IPC handle size");
+    std::memset(out, 0, 64);
+    std::memcpy(out, &h, sizeof(h));
+    return 0;
+}
+
+namespace {
+int upload_peers(grm_engine *e, const std::vector<const DevCounters *> &tab) {
+    hipFree(e->d_peers);
+    e->d_peers = nullptr;
+    e->n_peers = 0;
+    if (tab.size() < 2) return 0;
+    HIPCHK(e, hipMalloc(&e->d_peers, tab.size() * sizeof(DevCounters *)));
+    HIPCHK(e, hipMemcpy(e->d_peers, tab.data(), tab.size() * sizeof(DevCounters *), hipMemcpyHostToDevice));
+    e->n_peers = (int)tab.size();
+    return 0;
+}
+} /* namespace */
+
+int grm_engine_set_peers(grm_engine *e, const uint8_t *handles, int n, int rank) {
+    if (!e || n < 0 || (n > 1 && (!handles || rank < 0 || rank >= n))) return -1;
+    if (n > 64) {
+        e->err = "grm_engine_set_peers: at most 64 ranks";
+        return -1;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    for (void *p : e->ipc_open) hipIpcCloseMemHandle(p);
+    e->ipc_open.clear();
+    std::vector<const DevCounters *> tab;
+    if (n > 1) {
+        if (!e->d_ctr_slots) {
+            e->err = "grm_engine_set_peers: no pass slots (grm_engine_stash_reserve first)";
+            return -1;
+        }
+        for (int r = 0; r < n; ++r) {
+            if (r == rank) {
+                tab.push_back(e->d_ctr_slots);
+                continue;
+            }
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, handles + (size_t)r * 64, sizeof(h));
+            void *p = nullptr;
+            const hipError_t st = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+            if (st != hipSuccess) {
+                for (void *q : e->ipc_open) hipIpcCloseMemHandle(q);
+                e->ipc_open.clear();
+                e->err = std::string("grm_engine_set_peers: hipIpcOpenMemHandle of rank ") + std::to_string(r) + ": " +
+                         hipGetErrorString(st);
+                upload_peers(e, {});
+                return -1;
+            }
+            e->ipc_open.push_back(p);
+            tab.push_back(reinterpret_cast<const DevCounters *>(p));
+        }
+    }
+    return upload_peers(e, tab);
+}
+
+int grm_engine_link_peers(grm_engine *const *engines, int n) {
+    if (!engines || n < 1) return -1;
+    std::vector<const DevCounters *> tab;
+    for (int r = 0; r < n; ++r) {
+        if (!engines[r] || !engines[r]->d_ctr_slots || engines[r]->device != engines[0]->device) return -1;
+        tab.push_back(engines[r]->d_ctr_slots);
+    }
+    for (int r = 0; r < n; ++r) {
+        grm_engine *e = engines[r];
+        HIPCHK(e, hipSetDevice(e->device));
+        if (upload_peers(e, n > 1 ? tab : std::vector<const DevCounters *>{})) return -1;
+    }
+    return 0;
+}
+
+int grm_engine_job_counters(grm_engine *e, double out[4]) {
+    if (!e || !out) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    Ctl C{};
+    C.ctr = e->d_ctr;
+    C.peers = e->d_peers;
+    C.n_peers = (e->ctr_slot >= 0 && e->d_peers) ? e->n_peers : 0;
+    C.ctr_slot = e->ctr_slot;
+    double *d = nullptr;
+    HIPCHK(e, hipMalloc(&d, 4 * sizeof(double)));
+    hipLaunchKernelGGL(job_counters_kernel, dim3(1), dim3(64), 0, e->stream, e->P, C, d);
+    hipError_t st = hipGetLastError();
+    if (st == hipSuccess) st = hipMemcpyAsync(out, d, 4 * sizeof(double), hipMemcpyDeviceToHost, e->stream);
+    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    return hip_ok(e, st, "job counters") ? 0 : -1;
 }
 
 int grm_engine_stash(grm_engine *e, int slot) {

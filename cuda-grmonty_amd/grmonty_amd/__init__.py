@@ -134,6 +134,11 @@ SIGNATURES = {
                                         C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "grm_engine_stash_raw": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, VP, C.c_int]),
     "grm_stash_words": (C.c_int, [C.c_int]),
+    "grm_engine_begin_pass": (C.c_int, [VP, C.c_int]),
+    "grm_engine_counters_ipc_handle": (C.c_int, [VP, C.POINTER(C.c_uint8)]),
+    "grm_engine_set_peers": (C.c_int, [VP, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    "grm_engine_link_peers": (C.c_int, [C.POINTER(VP), C.c_int]),
+    "grm_engine_job_counters": (C.c_int, [VP, DP]),
     "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
     "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_stuck": (C.c_int64, [VP, VP, C.c_size_t]),
@@ -432,6 +437,27 @@ class Engine:
                                                  C.byref(st)))
         return spec.reshape(N_TH_BINS, N_E_BINS), nr.value, ns.value, mt.value, st.value
 
+    def begin_pass(self, slot: int):
+        """count the next pass into counter block `slot` (shared with the peers; reset first); -1 = the
+        engine's private block"""
+        self._check(self.L.grm_engine_begin_pass(self.h, int(slot)))
+
+    def counters_ipc_handle(self) -> bytes:
+        buf = (C.c_uint8 * 64)()
+        self._check(self.L.grm_engine_counters_ipc_handle(self.h, buf))
+        return bytes(buf)
+
+    def set_peers(self, handles: list, rank: int):
+        """the other ranks' counter blocks (their counters_ipc_handle(), rank order)"""
+        n = len(handles)
+        buf = (C.c_uint8 * (64 * max(n, 1))).from_buffer_copy(b"".join(handles) if n else bytes(64))
+        self._check(self.L.grm_engine_set_peers(self.h, buf, n, int(rank)))
+
+    def job_counters(self) -> dict:
+        o = np.zeros(4)
+        self._check(self.L.grm_engine_job_counters(self.h, o.ctypes.data_as(DP)))
+        return dict(bias_den=o[0], n_scatt=o[1], n_recorded=o[2], max_tau_scatt=o[3])
+
     def stash_raw(self, n_slots: int, first: int = 0):
         """(spectra [n, words0] f64, sums [n, words1] u64, maxs [n, words2] u64): the stash's raw
         words in the engine's packing (grm_engine_stash_raw)"""
@@ -493,6 +519,13 @@ def zone_shards(zone_weights: np.ndarray, world: int, mode: str = "strided") -> 
     if mode == "contiguous":
         return [(a, b, 1) for a, b in shard_zones(zone_weights, world)]
     raise ValueError(mode)
+
+
+def link_peers(engines: list):
+    """share the pass counter blocks of engines on one device in one process (N-rank emulation)"""
+    arr = (VP * len(engines))(*[e.h for e in engines])
+    if lib().grm_engine_link_peers(arr, len(engines)) != 0:
+        raise RuntimeError("grm_engine_link_peers failed")
 
 
 def rccl_unique_id() -> bytes:

@@ -250,6 +250,25 @@ int grm_engine_stash_raw(grm_engine *e, int first, int n_slots, double *spec, ui
                          int write);
 int grm_stash_words(int which);
 
+/* The job's adaptive bias across ranks.  bias_func (harm_model.cpp:1391-1404) runs on the counters
+ * of every photon recorded so far; a rank that saw only its own would run on a history N times
+ * shorter (measured: +18 / +30 / +35 % recorded at 2 / 4 / 8 emulated ranks).  Each
+ * engine keeps one counter block per pass slot (allocated by grm_engine_stash_reserve); with peers
+ * set, the transport kernels read the SAME slot of every rank's blocks (remote ones over xGMI) and
+ * run bias_func on their sums (max for max tau_scatt).
+ *   grm_engine_begin_pass(e, slot): the next pass counts into block `slot` (reset first); slot < 0
+ *     = the engine's private block, no sharing (the default).
+ *   grm_engine_counters_ipc_handle: the 64-byte IPC handle of this engine's blocks, for the others;
+ *   grm_engine_set_peers(e, handles[n][64], n, rank): open the other ranks' blocks (n <= 1: off);
+ *   grm_engine_link_peers(engines, n): the same for n engines of one process on one device.
+ *   grm_engine_job_counters(e, out[4]): bias_func's denominator, summed n_scatt, n_recorded and max
+ *     tau_scatt of the current slot as the kernels see them (diagnostics / tests). */
+int grm_engine_begin_pass(grm_engine *e, int slot);
+int grm_engine_counters_ipc_handle(grm_engine *e, uint8_t out[64]);
+int grm_engine_set_peers(grm_engine *e, const uint8_t *handles, int n, int rank);
+int grm_engine_link_peers(grm_engine *const *engines, int n);
+int grm_engine_job_counters(grm_engine *e, double out[4]);
+
 /* --- host model (harm_model.hpp; C++ host, no GPU) ------------------------------------- */
 typedef struct grm_model grm_model;
 /* HARMModel(photon_n, mass_unit) + read_file(path)   harm_model.cpp:64-232 */

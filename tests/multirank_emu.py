@@ -1,0 +1,99 @@
+"""N-rank job emulated on ONE GPU, ranks running concurrently (run as its own process, so that the
+HIP runtime starts with enough hardware queues for N concurrent engines: GPU_MAX_HW_QUEUES).
+
+Each emulated rank is an engine with 1/N of the CUs (GRM_OPT_GRID_BLOCKS), the zone shard bench.py
+gives rank r (grmonty_amd.zone_shards: every N-th zone from r), its global photon id base, and its
+own counter block per pass; with --shared the blocks are linked (grm_engine_link_peers), so every
+rank's adaptive bias runs on the job's counters as on N GPUs with grm_engine_set_peers.  The N
+passes of a seed start together from N host threads; the job's results are the ranks' sums.
+
+    python tests/multirank_emu.py DUMP WORLD SEEDS OUT.json [--shared] [--photon-n 1e5]
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(os.path.dirname(HERE), "cuda-grmonty_amd"), HERE]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dump")
+    ap.add_argument("world", type=int)
+    ap.add_argument("seeds", type=int)
+    ap.add_argument("out")
+    ap.add_argument("--shared", action="store_true")
+    ap.add_argument("--photon-n", type=float, default=1e5)
+    ap.add_argument("--seed0", type=int, default=123)
+    args = ap.parse_args()
+    import numpy as np
+    import grmonty_amd as G
+    world = args.world
+    model = G.Model.load(args.dump, photon_n=int(args.photon_n)).init(8, device=0)
+    shards = G.zone_shards(model.zone_weights(), world)
+    engines = []
+    for r in range(world):
+        e = G.Engine(model, device=0)
+        e.set_option(G.OPT_GRID_BLOCKS, max(1, 256 // world))
+        e.emit_setup(model)
+        e.stash_reserve(args.seeds)
+        engines.append(e)
+    if args.shared:
+        G.link_peers(engines)
+    res = []
+    for s in range(args.seeds):
+        seed = args.seed0 + s
+        counts = [model.count(seed=seed, z0=a, z1=b, stride=st) for a, b, st in shards]
+        out = [None] * world
+        err = []
+        go = threading.Barrier(world)
+
+        def rank(r):
+            try:
+                e = engines[r]
+                e.begin_pass(s)
+                e.set_option(G.OPT_SEED, seed)
+                e.set_option(G.OPT_ID_BASE, int(sum(counts[:r])))
+                a, b, st = shards[r]
+                go.wait()
+                p, n = e.emit(seed=seed, z0=a, z1=b, stride=st)
+                e.track_device(p, n)
+                stt = e.stats()
+                if stt["n_dropped"] or stt["n_abandoned"]:
+                    raise RuntimeError("photons lost")
+                spec, nr, ns, mt = e.finish()
+                out[r] = dict(spec=spec, created=n, recorded=nr, scattered=ns, steps=stt["n_steps"], max_tau=mt)
+            except Exception as ex:  # reported below
+                err.append(repr(ex))
+                go.abort()
+
+        th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            raise RuntimeError(err[0])
+        spec = out[0]["spec"].copy()
+        for o in out[1:]:
+            for f in spec.dtype.names:
+                spec[f] += o["spec"][f]
+        job = {k: int(sum(o[k] for o in out)) for k in ("created", "recorded", "scattered", "steps")}
+        job["luminosity"] = model.write_spectrum(spec, None)["luminosity"]
+        # every rank's view of the job's counters once all passes ended (the kernels' bias_den path):
+        # must be the sums of the ranks' own counters and the max of their max tau_scatt
+        job["max_tau"] = max(o["max_tau"] for o in out)
+        job["job_view"] = [e.job_counters() for e in engines] if args.shared else None
+        job["per_rank_recorded"] = [o["recorded"] for o in out]
+        res.append(job)
+        print(json.dumps({k: v for k, v in job.items() if k != "job_view"}), flush=True)
+    for e in engines:
+        e.close()
+    json.dump(res, open(args.out, "w"))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,13 +1,17 @@
 """The multi-GPU job on one MI355X.
 
 1. N-rank jobs emulated on one GPU (N = 2, 4, 8), live adaptive bias, against the oracle's
-   run_simulation at the headline scale (192x192, photon_n = 1e5; tests/golden/oracle_synth192_pn1e5.*):
-   each emulated rank runs bench.py's zone shard (grmonty_amd.zone_shards, strided: every N-th
-   zone) as a pass of its own after a reset, so its bias_func (harm_model.cpp:1391-1404) sees only
-   its own counters, as on N GPUs; the ranks' results are summed.  The job's counters are tested
-   the way the single-GPU job's are (tests/test_gpu_parity_192.py): the mean over N_DEV seeds
-   against the oracle's mean, and the KS test of one traced job.  (Contiguous zone ranges failed
-   this: +17 / +30 / +43 % recorded at 2 / 4 / 8 ranks, profiles/r03a_multirank_contiguous.log.)
+   run_simulation at the headline scale (192x192, photon_n = 1e5; tests/golden/oracle_synth192_pn1e5.*).
+   tests/multirank_emu.py runs N engines concurrently, each with 1/N of the CUs, bench.py's zone
+   shard (grmonty_amd.zone_shards: every N-th zone from r), its global id base and its per-pass
+   counter block, the blocks linked (grm_engine_link_peers: the kernels run bias_func on the job's
+   counters, harm_model.cpp:1391-1404, as grm_engine_set_peers makes them do across GPUs).  The job's
+   counters are tested as the single-GPU job's are (tests/test_gpu_parity_192.py): the mean over
+   N_DEV seeds against the oracle's mean, |diff| <= Z_MAX combined standard errors; and every rank's
+   view of the job counters (the kernels' own summation path) must equal the sums of the ranks'.
+   Without the link each rank's bias runs on its own history, N times shorter: +18 / +30 / +35 %
+   recorded at 2 / 4 / 8 ranks with strided shards (profiles/r03b_pytest_multirank_unshared.log),
+   +17 / +30 / +43 % with contiguous ones (profiles/r03a_multirank_contiguous.log).
 
 2. The multi-rank reduction on the engine's own stash buffers: two processes on the GPU, one engine
    each, run the two shards of a frozen-bias job (so the result is exact), stash their passes
@@ -26,8 +30,8 @@ import socket
 import numpy as np
 import pytest
 
-from job_util import KEYS, run_job
-from spectrum_stats import binned_ks, ks_crit, welch_z
+from job_util import KEYS
+from spectrum_stats import welch_z
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -36,51 +40,34 @@ N_DEV = 16
 Z_MAX = 4.5
 
 
-@pytest.fixture(scope="module")
-def setup192(dump_dir):
-    import grmonty_amd as GA
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_emulated_ranks_vs_oracle(dump_dir, tmp_path, world):
+    import subprocess
+    import sys
     from grmonty_amd.synth_dump import ensure_dump
     path = ensure_dump(os.path.join(dump_dir, "synth192.dump"), 192, 192)
-    model = GA.Model.load(path, photon_n=100000).init(8, device=0)  # the tables bench.py uses
-    eng = GA.Engine(model, device=0)
-    eng.emit_setup(model)
-    yield model, eng
-    eng.close()
-
-
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_emulated_ranks_vs_oracle(setup192, world):
-    import grmonty_amd as GA
-    model, eng = setup192
-    shards = GA.zone_shards(model.zone_weights(), world)
+    out = tmp_path / "emu.json"
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(min(32, 2 * world + 2)))
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "multirank_emu.py"), path, str(world), str(N_DEV),
+                        str(out), "--shared"], env=env, capture_output=True, text=True, timeout=280)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stderr[-3000:]
+    jobs = json.load(open(out))
     summ = json.load(open(GOLD + ".json"))
-    o = {k: np.array([r[k] for r in summ["runs"]], dtype=np.float64) for k in KEYS}
-    dev = {k: [] for k in KEYS}
-    per_rank = []
-    for s in range(N_DEV):
-        job = run_job(eng, model, 123 + s, shards=shards)
-        for k in KEYS:
-            dev[k].append(job[k])
-        per_rank.append([r["recorded"] / max(1, r["created"]) for r in job["per_rank"]])
-    print(f"{world} ranks, shards {shards}; recorded per created by rank (mean over seeds): "
-          f"{np.round(np.mean(per_rank, axis=0), 3).tolist()}")
+    o = {k: np.array([x[k] for x in summ["runs"]], dtype=np.float64) for k in KEYS}
     bad = []
     for k in KEYS:
-        diff, se, z = welch_z(dev[k], o[k])
-        print(f"{k:10s} device {np.mean(dev[k]):.6g} +- {np.std(dev[k], ddof=1):.3g} ({N_DEV} jobs)  oracle "
-              f"{o[k].mean():.6g} +- {o[k].std(ddof=1):.3g} ({len(o[k])} runs)  diff {diff / o[k].mean():+.2%} "
+        dev = [j[k] for j in jobs]
+        diff, se, z = welch_z(dev, o[k])
+        print(f"{world} ranks {k:10s} device {np.mean(dev):.6g} +- {np.std(dev, ddof=1):.3g} ({len(dev)} jobs)  "
+              f"oracle {o[k].mean():.6g} +- {o[k].std(ddof=1):.3g} ({len(o[k])} runs)  diff {diff / o[k].mean():+.2%} "
               f"= {z:+.2f} SE")
         if abs(z) > Z_MAX:
             bad.append((k, z))
-    # the spectrum's shape: one traced job against the pooled oracle runs
-    job = run_job(eng, model, 123, shards=shards, trace_cap=12_000_000)
-    pooled = np.load(GOLD + ".npz")["cells"].sum(axis=0)
-    for th in [None, 0, 1, 2, 3, 4, 5]:
-        d, n1, n2 = binned_ks(job["cells"], pooled, th)
-        crit = ks_crit(n1, n2, 1e-4)
-        print(f"theta bin {th}: KS D={d:.4f} crit={crit:.4f}")
-        if not d < crit:
-            bad.append(("ks", th, d, crit))
+    for j in jobs:
+        for v in j["job_view"]:
+            assert v["n_recorded"] == j["recorded"] and v["n_scatt"] == j["scattered"]
+            assert v["max_tau_scatt"] == j["max_tau"]
     assert not bad, bad
 
 
@@ -172,3 +159,59 @@ def test_gloo_reduction_of_engine_stash(dump64, tmp_path):
         assert raw[slot][3] == st["n_tracked"] and raw[slot][4] == st["n_children"] and raw[slot][7] == n
         np.testing.assert_allclose(spec_d[slot], spec1.view(np.float64).reshape(-1), rtol=1e-12, atol=0)
     eng.close()
+
+
+def _ipc_rank(rank, world, dump, out_dir, port):
+    """grm_engine_set_peers across processes: IPC handles of the pass counter blocks exchanged over
+    gloo, a live-bias pass on each rank, then every rank's kernel-side view of the job counters"""
+    import sys
+    sys.path[:0] = [os.path.join(os.path.dirname(HERE), "cuda-grmonty_amd"), HERE]
+    import torch
+    import torch.distributed as dist
+    import grmonty_amd as G
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    model = G.Model.load(dump, photon_n=3000).init(4)
+    shards = G.zone_shards(model.zone_weights(), world)
+    eng = G.Engine(model, device=0)
+    eng.emit_setup(model)
+    eng.stash_reserve(1)
+    handles = [None] * world
+    dist.all_gather_object(handles, eng.counters_ipc_handle())
+    eng.set_peers(handles, rank)
+    eng.begin_pass(0)
+    dist.barrier()
+    eng.set_option(G.OPT_SEED, 123)
+    eng.set_option(G.OPT_ID_BASE, sum(model.count(seed=123, z0=a, z1=b, stride=st) for a, b, st in shards[:rank]))
+    a, b, st = shards[rank]
+    p, n = eng.emit(seed=123, z0=a, z1=b, stride=st)
+    eng.track_device(p, n)
+    _, nr, ns, mt = eng.finish()
+    dist.barrier()  # both passes done
+    view = eng.job_counters()
+    own = torch.tensor([float(nr), float(ns)], dtype=torch.float64)
+    mx = torch.tensor([mt], dtype=torch.float64)
+    dist.all_reduce(own, op=dist.ReduceOp.SUM)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    json.dump(dict(view=view, rec=float(own[0]), scatt=float(own[1]), max_tau=float(mx[0]), own_rec=nr),
+              open(os.path.join(out_dir, f"ipc_{rank}.json"), "w"))
+    dist.barrier()
+    eng.set_peers([], 0)  # close the mapped blocks before the owners free them
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_ipc_peer_counters(dump64, tmp_path):
+    """two processes on the GPU: each maps the other's per-pass counter blocks by IPC
+    (grm_engine_counters_ipc_handle / grm_engine_set_peers), and the transport kernels' view of the
+    job counters equals the sums of both ranks' counters (max for max tau_scatt)"""
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_ipc_rank, args=(world, dump64, str(tmp_path), _free_port()), nprocs=world, join=True)
+    for r in range(world):
+        d = json.load(open(tmp_path / f"ipc_{r}.json"))
+        print(r, d)
+        assert d["view"]["n_recorded"] == d["rec"] and d["view"]["n_scatt"] == d["scatt"]
+        assert d["view"]["max_tau_scatt"] == d["max_tau"]
+        assert 0 < d["own_rec"] < d["rec"]
