@@ -1268,7 +1268,88 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
         ti[1] += (unsigned long long)nb;
         ti[2] += tb1 - tb0;
 #endif
-        for (int bj = 0; bj < nb; ++bj) {
+        /* The batch's leading run of PLAIN steps is committed at once: a step that interacts,
+         * neither stops, roulettes, scatters nor is absorbed changes the state only by w *= fac,
+         * tau += d_tau, one draw and the coefficients it leaves -- every lane decides its step from
+         * the weight before it (the sequential product, in the serial order, so bit-identical) and
+         * the draw at its counter; the first lane that is not plain ends the run, and its step (and
+         * the rest of the batch) goes through the serial code below. */
+        int bj0 = 0;
+        {
+            /* weight and optical depths before step j (lane j), and after all nb steps (lane nb) */
+            double w_run = w, ta_run = tau_abs, ts_run = tau_scatt;
+            double w_j = w, ta_j = tau_abs, ts_j = tau_scatt;
+            for (int j = 0; j < nb; ++j) {
+                if (lane == j) {
+                    w_j = w_run;
+                    ta_j = ta_run;
+                    ts_j = ts_run;
+                }
+                w_run = w_run * bcast(l_fac, j);
+                ta_run = ta_run + bcast(l_dta, j);
+                ts_run = ts_run + bcast(l_dts, j);
+            }
+            if (lane == nb) {
+                w_j = w_run;
+                ta_j = ta_run;
+                ts_j = ts_run;
+            }
+            /* the window of draws must hold counters rng.ctr .. rng.ctr + nb - 1 */
+            if (rng.ctr - wbase + (uint32_t)nb > 64u) {
+                wbase = rng.ctr;
+                Rng g = rng;
+                g.ctr = wbase + (uint32_t)lane;
+                win = uniform(g);
+            }
+            const double u = __shfl(win, (int)(rng.ctr - wbase) + (lane < nb ? lane : 0));
+            /* the state before step j: lane j - 1's results, or the carried ones for j = 0 */
+            const double up_x1 = __shfl_up(l_x1, 1), up_ne = __shfl_up(l_ne, 1);
+            const double up_as = __shfl_up(l_as, 1), up_aa = __shfl_up(l_aa, 1);
+            const double x1_prev = lane == 0 ? x1 : up_x1;
+            const double ne_prev = lane == 0 ? fl_ne : up_ne, as_prev = lane == 0 ? a_si : up_as,
+                         aa_prev = lane == 0 ? a_ai : up_aa;
+            /* bias_func with the weight cap (:1391-1404) and the interaction's bias (:977) */
+            double bf = 0.0;
+            if (!l_zero) {
+                const double max = w_j * (0.5 / WEIGHT_MIN);
+                double b = l_b0;
+                if (b > max) b = max;
+                bf = b * (1.0 / TP_OVER_TE);
+            }
+            const double up_bf = __shfl_up(bf, 1);
+            const double bi_prev = lane == 0 ? bi : up_bf;
+            const double bias = l_zero ? 0.0 : 0.5 * (bi_prev + bf);
+            const double bdt = bias * l_dts;
+            const bool may = bdt > (1.0 - u) * (1.0 - 0x1p-40);
+            const double lx = may ? -flog(u) : 0.0;
+            bool scatter = may && bdt > lx;
+            if (scatter) scatter = fdiv(w_j, bias) > WEIGHT_MIN;
+            const bool plain = lane < nb && !(x1_prev < P.x1_min) && !(x1_prev > P.x1_max) && !(w_j < WEIGHT_MIN) &&
+                               !(l_x1 < P.x1_min) && !(l_x1 > P.x1_max) && !isnan(l_x1) &&
+                               (aa_prev > 0.0 || as_prev > 0.0 || ne_prev > 0.0) && !scatter && !(l_dta > 100) &&
+                               n_step + lane + 1 <= MAX_N_STEP;
+            const unsigned long long np = __ballot(!plain);
+            bj0 = np ? __ffsll((long long)np) - 1 : 64; /* lanes >= nb are not plain: bj0 <= nb */
+            if (bj0 > 0) {
+                const int l = bj0 - 1;
+                w = bcast(w_j, bj0);
+                tau_abs = bcast(ta_j, bj0);
+                tau_scatt = bcast(ts_j, bj0);
+                x1 = bcast(l_x1, l);
+                fl_ne = bcast(l_ne, l);
+                a_si = bcast(l_as, l);
+                a_ai = bcast(l_aa, l);
+                bi = bcast(bf, l);
+                rng.ctr += (uint32_t)bj0;
+                n_step += bj0;
+                steps += (unsigned long long)bj0;
+                since += (unsigned)bj0;
+                cur = base + (unsigned long long)l;
+                si = base + (unsigned long long)bj0;
+                if (own) __hip_atomic_store(&pr.ctl.cons, si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        for (int bj = bj0; bj < nb; ++bj) {
             ++since;
             /* while (!stop_criterion(photon)) (:919) */
             if (lone_stop(P, x1, w, rng, win, wbase, lane)) {

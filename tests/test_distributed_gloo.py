@@ -43,7 +43,12 @@ def pack_counters(orc) -> np.ndarray:
     return v
 
 
-def _shard_job(rank, world, dump, out_dir, port):
+def job_photon_n(world, scaling):
+    """bench.py's job size: photon_n per GPU (weak) or for the whole job (strong)"""
+    return 150 * world if scaling == "weak" else 300
+
+
+def _shard_job(rank, world, dump, out_dir, port, photon_n):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.join(os.path.dirname(here), "cuda-grmonty_amd"), os.path.join(os.path.dirname(here), "oracle")]
@@ -51,12 +56,12 @@ def _shard_job(rank, world, dump, out_dir, port):
     import oracle_py as O
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    model = G.Model.load(dump, photon_n=150 * world).init(2)
+    model = G.Model.load(dump, photon_n=photon_n).init(2)
     shards = G.zone_shards(model.zone_weights(), world)
     counts = [model.count(seed=123, z0=a, z1=b, stride=st) for a, b, st in shards]
     a, b, st = shards[rank]
     ph = model.emit(seed=123, z0=a, z1=b, stride=st)
-    orc = O.OracleModel(dump, photon_n=150 * world)
+    orc = O.OracleModel(dump, photon_n=photon_n)
     orc.init(2)
     orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=123, id_base=int(sum(counts[:rank])), frozen=True,
               scatt0=SNAP["scatt"], rec0=SNAP["rec"], max_tau0=SNAP["maxtau"])
@@ -75,19 +80,23 @@ def _shard_job(rank, world, dump, out_dir, port):
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_equal_single_job(dump32, tmp_path):
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_two_rank_shards_equal_single_job(dump32, tmp_path, scaling):
+    """bench.py --scaling weak (photon_n per GPU) and strong (photon_n for the job): the ranks'
+    strided shards reduce to exactly the single-process job"""
     import grmonty_amd as G
     import oracle_py as O
     world = 2
-    mp.spawn(_shard_job, args=(world, dump32, str(tmp_path), _free_port()), nprocs=world, join=True)
+    pn = job_photon_n(world, scaling)
+    mp.spawn(_shard_job, args=(world, dump32, str(tmp_path), _free_port(), pn), nprocs=world, join=True)
     spec_d = np.load(tmp_path / "spec.npy")
     ctr_d = np.load(tmp_path / "ctr.npy")
-    model = G.Model.load(dump32, photon_n=150 * world).init(2)
+    model = G.Model.load(dump32, photon_n=pn).init(2)
     # the ranks' photons in rank order: the ids they were tracked under
     ph = np.concatenate([model.emit(seed=123, z0=a, z1=b, stride=st)
                          for a, b, st in G.zone_shards(model.zone_weights(), world)])
     assert len(ph) == model.count(seed=123)  # the shards' union is the single-GPU photon set
-    orc = O.OracleModel(dump32, photon_n=150 * world)
+    orc = O.OracleModel(dump32, photon_n=pn)
     orc.init(2)
     orc.track(ph.view(O.INIT_PHOTON), rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=SNAP["scatt"],
               rec0=SNAP["rec"], max_tau0=SNAP["maxtau"])
