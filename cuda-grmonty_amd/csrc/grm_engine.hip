@@ -2330,7 +2330,9 @@ struct grm_engine {
     int grid_override = 0;
     double max_tau_init = 0.0;
     bool frozen_set = false;
-    int64_t warmup = 4096;   /* photons; -1 = lanes (sweep: profiles/r02i_warmup_sweep.log) */
+    /* photons; -1 = lanes; -2 (default) = auto: lanes for a call of fewer than WARMUP_AUTO_RATIO x lanes
+     * photons, else WARMUP_PHOTONS (profiles/r03d_warmup_rank_sweep_1e5.log) */
+    int64_t warmup = -2;
     int warmup_slack = 4;
     int refill_min = 2;      /* primaries: set-up is in the trip (phase 3), so refill early */
     int child_min = 8;       /* children: batch the divergent scattering sampling */
@@ -2468,6 +2470,16 @@ int ensure_ovf(grm_engine *e, unsigned long long cap) {
     return 0;
 }
 
+/* Live-bias warm-up size (GRM_OPT_WARMUP = -2, the default).  The counters bias_func reads lag the
+ * claims by the photons in flight (~lanes): while the history is short against that, photons start
+ * on a bias the serial reference never had.  A call of fewer than WARMUP_AUTO_RATIO x lanes photons
+ * (photon_n = 1e5 on one GPU: 11 x lanes) ramps admission until the history reaches a grid's worth
+ * of lanes: recorded +6.1 % -> +1.8 % against the oracle at 192^2, photon_n = 1e5, for +73 ms per
+ * pass (16 seeds, profiles/r03d_warmup_rank_sweep_1e5.log; 16 k and 64 k photons did not move it).
+ * A larger call (the bench's photon_n = 1e6: 110 x lanes) keeps WARMUP_PHOTONS: its lag is ~1 % of
+ * the pass, and the ramp would cost ~15 % of it. */
+constexpr uint64_t WARMUP_AUTO_RATIO = 32, WARMUP_PHOTONS = 4096;
+
 /* one launch (+ overflow relaunches) over claim positions [pos0, pos1) of a batch of n primaries
  * interleaved as 2^sh runs of m (Ctl.pos_end) */
 int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, uint64_t m, uint64_t pos0,
@@ -2523,7 +2535,10 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
-        const uint64_t limit = e->warmup < 0 ? (uint64_t)e->lanes : (uint64_t)e->warmup;
+        const uint64_t n_call = pos1 - pos0;
+        const uint64_t limit = e->warmup == -2 ? (n_call < WARMUP_AUTO_RATIO * e->lanes ? (uint64_t)e->lanes : WARMUP_PHOTONS)
+                               : e->warmup < 0 ? (uint64_t)e->lanes
+                                               : (uint64_t)e->warmup;
         C.admit_n = (!e->bias_mode && e->history < limit && pos0 == 0) ? std::min<uint64_t>(pos1, limit - e->history) : 0;
         C.admit_h0 = e->history;
         C.admit_lim = limit;

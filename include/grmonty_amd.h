@@ -138,9 +138,10 @@ enum {
     /* live-bias warm-up: until this many photons have been claimed since the last reset, they are
      * admitted in batches that double the history each time (the next batch once all but a
      * 2^-GRM_OPT_WARMUP_SLACK fraction of the history has ended), so the adaptive-bias counters
-     * evolve as in the serial reference (default 4096; -1 = one persistent grid's worth of lanes;
-     * 0 = off).  Tuned by the reference-semantics counters at 192^2: 0 doubles the
-     * recorded / scattered counts, 2048..32768 all land within the oracle's seed spread, and each
+     * evolve as in the serial reference (default -2 = auto: one persistent grid's worth of lanes for
+     * a call of fewer than 32 x lanes photons, else 4096; -1 = lanes; 0 = off; n = n photons).
+     * Tuned by the reference-semantics counters at 192^2: 0 doubles the recorded /
+     * scattered counts; at photon_n = 1e5, 4096 leaves them +6 %, a grid's worth +2 %; each
      * doubling costs a batch barrier (~5-10 ms) per pass */
     GRM_OPT_WARMUP = 8,
     /* idle lanes a wavefront gathers before it takes emitted photons (1..64, default 2) */

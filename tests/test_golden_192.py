@@ -11,14 +11,16 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 from spectrum_stats import binned_ks, ks_crit
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-G = os.path.join(HERE, "golden", "oracle_synth192_pn1e5")
+FIXTURES = [os.path.join(HERE, "golden", f"oracle_synth192_{p}") for p in ("pn1e5", "pn1e6")]
 
 
-def test_oracle_seeds_pass_binned_ks():
+@pytest.mark.parametrize("G", FIXTURES, ids=["pn1e5", "pn1e6"])
+def test_oracle_seeds_pass_binned_ks(G):
     g = np.load(G + ".npz")
     cells = g["cells"]
     worst, over, tot = 0.0, 0, 0
@@ -35,7 +37,8 @@ def test_oracle_seeds_pass_binned_ks():
     assert over <= max(2, 0.01 * tot)
 
 
-def test_fixture_consistency():
+@pytest.mark.parametrize("G", FIXTURES, ids=["pn1e5", "pn1e6"])
+def test_fixture_consistency(G):
     g = np.load(G + ".npz")
     s = json.load(open(G + ".json"))
     cnt = g["counters"]  # created, scattered, recorded, steps

@@ -92,3 +92,45 @@ def test_headline_counter_means_vs_oracle(setup192):
         if abs(z) > Z_MAX:
             bad.append((k, z))
     assert not bad, bad
+
+
+G6 = os.path.join(HERE, "golden", "oracle_synth192_pn1e6")
+N_DEV6 = 8
+
+
+def test_bench_config_vs_oracle(dump_dir):
+    """The bench's own configuration (BASELINE configs[1]): photon_n = 1e6 on the 192^2 dump, tables
+    built on the GPU, as bench.py runs it, against six oracle run_simulation runs at photon_n = 1e6
+    (tests/golden/oracle_synth192_pn1e6.*, ~1 h of CPU each): the binned KS test of one traced pass
+    and the counter means of N_DEV6 passes (Welch, |diff| <= Z_MAX standard errors)."""
+    import grmonty_amd as GA
+    from grmonty_amd.synth_dump import ensure_dump
+    path = ensure_dump(os.path.join(dump_dir, "synth192.dump"), 192, 192)
+    model = GA.Model.load(path, photon_n=1_000_000).init(8, device=0)
+    eng = GA.Engine(model, device=0)
+    eng.emit_setup(model)
+    summ = json.load(open(G6 + ".json"))
+    o = {k: np.array([r[k] for r in summ["runs"]], dtype=np.float64) for k in KEYS}
+    dev = {k: [] for k in KEYS}
+    job = None
+    for s in range(N_DEV6):
+        j = run_job(eng, model, 123 + s, trace_cap=40_000_000 if s == 0 else 0)
+        job = j if s == 0 else job
+        for k in KEYS:
+            dev[k].append(j[k])
+    eng.close()
+    bad = []
+    for k in KEYS:
+        diff, se, z = welch_z(dev[k], o[k])
+        print(f"1e6 {k:10s} device {np.mean(dev[k]):.6g} +- {np.std(dev[k], ddof=1):.3g} ({N_DEV6} passes)  oracle "
+              f"{o[k].mean():.6g} +- {o[k].std(ddof=1):.3g} ({len(o[k])} runs)  diff {diff / o[k].mean():+.2%} = {z:+.2f} SE")
+        if abs(z) > Z_MAX:
+            bad.append((k, z))
+    pooled = np.load(G6 + ".npz")["cells"].sum(axis=0)
+    for th in [None, 0, 1, 2, 3, 4, 5]:
+        d, n1, n2 = binned_ks(job["cells"], pooled, th)
+        crit = ks_crit(n1, n2, 1e-4)
+        print(f"1e6 theta bin {th}: KS D={d:.4f} crit={crit:.4f} n_eff device {n1:.0f} oracle {n2:.0f}")
+        if not d < crit:
+            bad.append(("ks", th, d, crit))
+    assert not bad, bad
