@@ -533,54 +533,6 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
     return push_finish(C, k, kp, dk, dl, e_0_s, G.g00, G.g01, G.g03, e_1);
 }
 
-/* push_attempt for a wave whose lanes all hold the same push state (the lone pipeline's geometry
- * wave): the same operations and roundings, with the connection contracted over the lanes.  Lane l
- * forms row l & 3 of the connection only (four divergent blocks: the connection's instructions are
- * issued once, as in push_attempt) and contracts it with kc -- geo_rhs's expression -- so one
- * contraction per corrector pass instead of four; lanes 0..3 hand dk^0..3 to every lane by
- * v_readlane.  Bit-identical to push_attempt. */
-__device__ __forceinline__ double rows_bcast(double v, int src) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, src), hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ bool push_attempt_rows(const Params &P, double x[4], double k[4], double dk[4], double e_0_s,
-                                                  double dl, double &e_1, int lane) {
-    double kp[4];
-    push_kick(x, k, dk, dl, kp);
-    Trig T;
-    trig_at(P, x, T);
-    ConnPre Q;
-    connection_pre(P, T, Q);
-    double L[10];
-    connection_row(Q, lane & 3, L);
-    Gcov G;
-    gcov_from_trig(P, T, G);
-    const double dl_2 = 0.5 * dl;
-    double err;
-    int iter = 0;
-    do {
-        ++iter;
-        const double kc[4] = {kp[0], kp[1], kp[2], kp[3]};
-        /* geo_rhs (same expression) with this lane's row */
-        double d = -2.0 * (kc[0] * (L[1] * kc[1] + L[2] * kc[2] + L[3] * kc[3]) + kc[1] * (L[5] * kc[2] + L[6] * kc[3]) +
-                           L[8] * kc[2] * kc[3]);
-        d -= (L[0] * kc[0] * kc[0] + L[4] * kc[1] * kc[1] + L[7] * kc[2] * kc[2] + L[9] * kc[3] * kc[3]);
-        err = 0.0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            dk[i] = rows_bcast(d, i);
-            kp[i] = k[i] + dl_2 * dk[i];
-            err += fratio_tol(kc[i] - kp[i], kp[i] + EPS);
-        }
-    } while (err > E_TOL && iter < MAX_ITER);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) k[i] = kp[i];
-    e_1 = -(k[0] * G.g00 + k[1] * G.g01 + k[3] * G.g03);
-    const bool err_e = fabs(e_1 - e_0_s) > 1.0e-4 * fabs(e_0_s);
-    return (err_e || err > E_TOL || isnan(err) || isinf(err));
-}
-
 /* Per-lane spill slot for the push backup, laid out [component][lane] so that a wave's
  * accesses are consecutive 8-B words (conflict-free ds_read_b64 / ds_write_b64).  The
  * transport kernel points it at LDS; the probe kernel at a private array. */

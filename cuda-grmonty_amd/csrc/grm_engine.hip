@@ -1023,13 +1023,9 @@ __device__ void lone_geometry(const Params &P, const Ctl &C, int lane, LonePair 
                         dkb[i] = dk[i];
                     }
                     double e_1;
-#ifdef GRM_X_NOROWS /* experiment: the per-lane push (A/B of push_attempt_rows) */
                     Trig T;
                     Gcov G;
                     fail = push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
-#else
-                    fail = push_attempt_rows(P, x, k, dk, e_0_s, dl, e_1, lane);
-#endif
                     if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {

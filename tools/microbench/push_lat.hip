@@ -72,7 +72,6 @@ __global__ __launch_bounds__(64) void lat_kernel(Params P, const double *s, doub
             Gcov G; gcov_from_trig(P, T, G); double e1;
             bool f = push_finish_spec(C, k, kp, dk, dl, e0, G.g00, G.g01, G.g03, e1);
             r = e1 + k[0] + x[1] + dk[2] + (f ? 1.0 : 0.0); }
-        else if (WHAT == 8) { double e1; bool f = push_attempt_rows(P, x, k, dk, e0, dl, e1, (int)(threadIdx.x & 63)); r = e1 + k[0] + x[1] + dk[2] + (f ? 1.0 : 0.0); }
         else { /* corrector iteration count of the state: 1 or 2 */
             double e1; Trig T; Gcov G; double kp[4]; push_kick(x, k, dk, dl, kp); trig_at(P, x, T); Conn C; connection(P, T, C);
             double kc[4] = {kp[0], kp[1], kp[2], kp[3]}, err = 0.0;
@@ -164,15 +163,14 @@ int main() {
         hipLaunchKernelGGL(lat_kernel<5>, dim3(1), dim3(64), 0, 0, P, s, o, cyc, n);
         hipLaunchKernelGGL(lat_kernel<6>, dim3(1), dim3(64), 0, 0, P, s, o, cyc, n);
         hipLaunchKernelGGL(lat_kernel<7>, dim3(1), dim3(64), 0, 0, P, s, o, cyc, n);
-        hipLaunchKernelGGL(lat_kernel<8>, dim3(1), dim3(64), 0, 0, P, s, o, cyc, n);
         hipDeviceSynchronize();
     }
     hipMemcpy(c, cyc, sizeof c, hipMemcpyDeviceToHost);
-    const char *nm[9] = {"trig_at", "trig+conn(3 used)", "push_attempt", "step_size", "trig+conn(40)", "kick..metric",
-                         "push_spec2", "iterations", "push_attempt_rows"};
+    const char *nm[8] = {"trig_at", "trig+conn(3 used)", "push_attempt", "step_size", "trig+conn(40)", "kick..metric",
+                         "push_spec2", "iterations"};
     double oh[16];
     hipMemcpy(oh, o, sizeof oh, hipMemcpyDeviceToHost);
-    for (int w = 0; w < 9; ++w) if (w != 7) printf("%-18s %8.1f cycles (s_memtime) %8.1f ns per evaluation, one wave\n", nm[w], (double)c[w] / n, c[20 + w] * 10.0 / n);
+    for (int w = 0; w < 8; ++w) if (w != 7) printf("%-18s %8.1f cycles (s_memtime) %8.1f ns per evaluation, one wave\n", nm[w], (double)c[w] / n, c[20 + w] * 10.0 / n);
     printf("corrector passes of the test state: %.0f\n", oh[7] / n);
     for (int nw = 1; nw <= 4; ++nw) {
         hipLaunchKernelGGL(pair_kernel, dim3(1), dim3(64 * nw), 0, 0, P, s, o, cyc, n);
