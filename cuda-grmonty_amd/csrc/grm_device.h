@@ -191,10 +191,27 @@ struct Params {
     double jnu_l_min_t, jnu_d_l_t;
     double spec_l_e_0, th_dx2;
     double i_dx1, i_dx2, hc_i_d_l_w, hc_i_d_l_t, jnu_i_d_l_t; /* host reciprocals of the uniform divisors */
+    /* uniform factors of the metric / connection, formed on the host with the device expressions'
+     * own operations and order (so the same bits): a^2, a^3, a^4, 1 - h, (1 - h) pi, (1 - h) / (2 pi),
+     * (-2 pi pi)(1 - h), -2 a -- fp64 arithmetic on uniform values still costs VALU issue slots */
+    double a2, a3, a4, hs1, hs1_pi, th_fac, d2k, m2a;
     const double *zones;    /* [n1*n2][8]: rho,u,u1,u2,u3,B1,B2,B3 (64 B per zone) */
     const double *hotcross; /* [221][81] log10 sigma */
     const double *k2;       /* [201] log K2 */
 };
+
+/* the metric's uniform factors of Params from P.a and P.h_slope (host) */
+inline void params_metric(Params &P) {
+    const double a = P.a, h = P.h_slope;
+    P.a2 = a * a;
+    P.a3 = P.a2 * a;
+    P.a4 = P.a3 * a;
+    P.hs1 = 1.0 - h;
+    P.hs1_pi = P.hs1 * kPi;
+    P.th_fac = P.hs1 / (2.0 * kPi);
+    P.d2k = -2.0 * kPi * kPi * P.hs1;
+    P.m2a = -2.0 * a;
+}
 
 /* ------------------------------------------------------------------------- */
 /* Philox4x32-10 per-photon streams (counter = (draw index, photon id))       */
@@ -280,7 +297,7 @@ struct Trig {
 __device__ __forceinline__ void trig_at(const Params &P, const double x[4], Trig &T) {
     T.r1 = fexp(x[1]);
     fsincospi(2.0 * x[2], T.s2x, T.c2x);
-    fsincospi(x[2] + ((1.0 - P.h_slope) / (2.0 * kPi)) * T.s2x, T.sth, T.cth);
+    fsincospi(x[2] + P.th_fac * T.s2x, T.sth, T.cth); /* th_fac = (1 - h) / (2 pi) */
 }
 
 /* non-zero g_mu,nu of MKS Kerr + g^{00}, g^{01} (g^{02} = g^{03} = 0) */
@@ -295,18 +312,18 @@ __device__ __forceinline__ void gcov_from_trig(const Params &P, const Trig &T, G
     const double sin_theta = fabs(T.sth) + EPS;
     const double cos_theta = T.cth;
     const double s2 = sin_theta * sin_theta;
-    const double rho2 = r * r + a * a * cos_theta * cos_theta;
+    const double rho2 = r * r + P.a2 * cos_theta * cos_theta;
     const double rfac = r - P.r0;
-    const double hfac = kPi + (1.0 - P.h_slope) * kPi * T.c2x;
+    const double hfac = kPi + P.hs1_pi * T.c2x; /* pi + (1 - h) pi cos(2 pi x2) */
     const double irho2 = frcp(rho2);
     const double two_r_rho2 = 2.0 * r * irho2;
     G.g00 = (-1.0 + two_r_rho2);
     G.g01 = two_r_rho2 * rfac;
-    G.g03 = -2.0 * a * r * s2 * irho2;
+    G.g03 = P.m2a * r * s2 * irho2; /* -2 a r sin^2 / rho^2 */
     G.g11 = (1.0 + two_r_rho2) * rfac * rfac;
     G.g13 = (-a * s2 * (1.0 + two_r_rho2)) * rfac;
     G.g22 = rho2 * hfac * hfac;
-    G.g33 = s2 * (rho2 + a * a * s2 * (1.0 + two_r_rho2));
+    G.g33 = s2 * (rho2 + P.a2 * s2 * (1.0 + two_r_rho2));
     G.gn00 = -1.0 - 2.0 * r * irho2;
     G.gn01 = 2.0 * irho2;
 }
@@ -344,15 +361,14 @@ struct ConnPre {
 
 __device__ __forceinline__ void connection_pre(const Params &P, const Trig &T, ConnPre &Q) {
     const double r1 = T.r1, r2 = r1 * r1, r3 = r2 * r1, r4 = r3 * r1;
-    const double hs = P.h_slope;
-    const double dthdx2 = kPi * (1.0 + (1.0 - hs) * T.c2x);
-    const double d2thdx22 = -2.0 * kPi * kPi * (1.0 - hs) * T.s2x;
+    const double dthdx2 = kPi * (1.0 + P.hs1 * T.c2x);
+    const double d2thdx22 = P.d2k * T.s2x; /* -2 pi^2 (1 - h) sin(2 pi x2) */
     const double dthdx22 = dthdx2 * dthdx2;
     const double sth = T.sth, cth = T.cth;
     const double sth2 = sth * sth, r1sth2 = r1 * sth2, sth4 = sth2 * sth2;
     const double cth2 = cth * cth, cth4 = cth2 * cth2;
     const double s2th = 2.0 * sth * cth, c2th = 2.0 * cth2 - 1.0;
-    const double a = P.a, a2 = a * a, a3 = a2 * a, a4 = a3 * a;
+    const double a = P.a, a2 = P.a2, a3 = P.a3, a4 = P.a4;
     const double a2sth2 = a2 * sth2, a2cth2 = a2 * cth2, a4cth4 = a4 * cth4;
     const double rho2 = r2 + a2cth2, rho22 = rho2 * rho2, rho23 = rho22 * rho2;
     const double irho2 = frcp(rho2), irho22 = irho2 * irho2, irho23 = irho22 * irho2;

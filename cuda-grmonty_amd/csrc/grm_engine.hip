@@ -2841,6 +2841,7 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     P.hc_i_d_l_w = 1.0 / P.hc_d_l_w;
     P.hc_i_d_l_t = 1.0 / P.hc_d_l_t;
     P.jnu_i_d_l_t = 1.0 / P.jnu_d_l_t;
+    params_metric(P);
     P.zones = e->d_zones;
     P.hotcross = e->d_hot;
     P.k2 = e->d_k2;

@@ -145,6 +145,7 @@ __global__ __launch_bounds__(256) void foreign_kernel(Params P, const double *s,
 int main() {
     Params P{};
     P.a = 0.9375; P.h_slope = 0.3; P.r0 = 0.0; P.xs1 = 0.3; P.xe2 = 1.0;
+    params_metric(P);
     /* a photon near r = 6 M off the pole: x, k (k^0 from the null condition approx), dk/dlambda */
     double h[14] = {0.0, 1.79, 0.21, 0.4, 1.0, 0.12, 0.03, 0.05, 0.0, 0.0, 0.0, 0.0, -0.9, 0.01};
     double *s, *o; unsigned long long *cyc;
