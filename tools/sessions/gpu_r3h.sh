@@ -1,9 +1,9 @@
 #!/bin/bash
-# lone pipeline latency (one long photon alone in lone_kernel): current tree vs a built revision
+# Round-3 session h: BASELINE configs[4] (512^2) and configs[2] (photon_n = 1e7) bench lines on the final kernels.
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R" && mkdir -p gpurun_out
-for v in cur base; do
-  echo "== $v"
-  GRMONTY_AMD_LIB="$R/cuda-grmonty_amd/variants/libgrmonty_amd_v$v.so" timeout -k 10 200 python -u tools/lone_bench.py 20000 5 > gpurun_out/r3h_$v.log 2>&1 || { tail -5 gpurun_out/r3h_$v.log; exit 1; }
-  grep rep gpurun_out/r3h_$v.log
-done
+T=r3h
+timeout -k 10 400 python -u bench.py --grid 512 --steps 5 --warmup 1 --cpu-seconds 0 --overlap 0 > gpurun_out/${T}_bench_grid512.json 2> gpurun_out/${T}_bench_grid512.err || { tail -5 gpurun_out/${T}_bench_grid512.err; exit 1; }
+tail -c 400 gpurun_out/${T}_bench_grid512.json
+timeout -k 10 500 python -u bench.py --photon-n 1e7 --steps 3 --warmup 1 --cpu-seconds 0 --overlap 0 > gpurun_out/${T}_bench_pn1e7.json 2> gpurun_out/${T}_bench_pn1e7.err || { tail -5 gpurun_out/${T}_bench_pn1e7.err; exit 1; }
+tail -c 400 gpurun_out/${T}_bench_pn1e7.json
 rm -f gpurun_out/*.dump
