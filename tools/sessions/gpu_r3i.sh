@@ -1,6 +1,5 @@
 #!/bin/bash
-# transport + parity tests on the current tree, then the lone latency probe
+# Round-3 session i: what the live-bias warm-up costs inside the dominant launch at photon_n = 1e6
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R" && mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_transport.py tests/test_gpu_parity_192.py > gpurun_out/r3i_pytest.log 2>&1 || { tail -20 gpurun_out/r3i_pytest.log; exit 1; }
-grep -E "PASS|FAIL" gpurun_out/r3i_pytest.log | cut -c1-120
-bash tools/sessions/gpu_r3h.sh
+OPTS="base 8=0 8=1024 14=512 8=16384" ROUNDS=2 STEPS=5 TAG=r3i bash tools/ab_opts.sh || exit 1
+rm -f gpurun_out/*.dump
