@@ -132,6 +132,7 @@ struct Ctl {
     LoneRec *lone;
     unsigned long long lone_cap, *lone_count;
     int lone_all;
+    int lone_k; /* the pool drained and the stack empty, a wave with <= lone_k photons hands them all over */
     /* early hand-over of long photons to the concurrent early_kernel (early_q null = off): a photon
      * of >= early_steps steps at the top of a step; slots claimed by *early_tail, published by
      * early_ready[slot] = early_tag; *wg_exit counts exited workgroups, the last sets *early_done;
@@ -866,6 +867,7 @@ __device__ __forceinline__ void push_overflow(const Ctl &C, const double x[4], c
  * itself and restarts the geometry wave from it (a new generation; steps of the old one are
  * discarded by their tag).  Both halves of a step then run at once on two SIMDs. */
 constexpr int LONE_RING = 32, LONE_BATCH = 16;
+constexpr int LONE_K_MAX = 16; /* hand-overs per wave at the end of a launch (GRM_OPT_LONE_K) */
 constexpr unsigned long long LONE_STOP = ~0ull;
 struct alignas(16) LoneSlot {
     double out[13], dl;     /* the state after the push (x, k, dk/dlambda, e_0_s) and the step size */
@@ -2096,8 +2098,9 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         const bool tail = pool_done && !warm;
         if (tail || C.lone_all) {
             const unsigned long long act = __ballot(active);
-            const bool alone = __popcll(act) == 1 && *wtop == 0;
-            if (C.lone && (alone || C.lone_all)) {
+            const int n_act = __popcll(act);
+            const bool alone = n_act == 1 && *wtop == 0;
+            if (C.lone && ((n_act <= C.lone_k && *wtop == 0) || C.lone_all)) {
                 const bool hand = active && L.phase == 0;
                 if (__ballot(hand)) {
                     unsigned long long slot = ~0ull;
@@ -2351,6 +2354,7 @@ struct grm_engine {
     LoneRec *d_lone = nullptr;             /* photons handed over to lone_kernel */
     unsigned long long lone_cap = 0;
     int lone = 1;                          /* GRM_OPT_LONE */
+    int lone_k = 1;                        /* GRM_OPT_LONE_K */
     /* early hand-over of long photons to early_kernel on a second stream (GRM_OPT_EARLY_STEPS) */
     int early_steps = 5000;
     bool early_serial = false; /* test: the worker ahead of the main launch on its stream */
@@ -2447,7 +2451,7 @@ int alloc_lanes(grm_engine *e) {
          * mode GRM_OPT_LONE = 2, sized in run_passes) */
         if (e->d_lone) (void)hipFree(e->d_lone);
         e->d_lone = nullptr;
-        e->lone_cap = lanes / 64;
+        e->lone_cap = lanes / 64 * LONE_K_MAX;
         HIPCHK(e, hipMalloc(&e->d_lone, e->lone_cap * sizeof(LoneRec)));
         e->lanes = lanes;
     }
@@ -2527,6 +2531,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.lone_cap = e->lone_cap;
     C.lone_count = e->d_small + 7;
     C.lone_all = e->lone == 2;
+    C.lone_k = e->lone_k;
     C.karg_test = e->karg_test;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
@@ -2934,6 +2939,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
+    case GRM_OPT_LONE_K: e->lone_k = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }

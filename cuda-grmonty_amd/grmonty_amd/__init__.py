@@ -53,6 +53,7 @@ OPT_WARMUP_BATCH = 14
 OPT_EARLY_STEPS = 15
 OPT_EARLY_SERIAL = 16
 OPT_KARG_TEST = 17
+OPT_LONE_K = 18
 N_TH_BINS, N_E_BINS = 6, 200
 
 

@@ -171,7 +171,11 @@ enum {
     GRM_OPT_EARLY_SERIAL = 16,
     /* test only: != 0 makes the transport kernel's kernel-argument check fail (the failure path must
      * end the call with an error, no photon tracked) */
-    GRM_OPT_KARG_TEST = 17
+    GRM_OPT_KARG_TEST = 17,
+    /* with GRM_OPT_LONE = 1: once the pool is drained, a wave whose stack is empty and that holds at
+     * most this many photons (1..64, default 1) hands them all to two-wave pairs of the lone kernel
+     * instead of stepping them in a nearly empty lane loop */
+    GRM_OPT_LONE_K = 18
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
