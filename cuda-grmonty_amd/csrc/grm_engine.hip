@@ -2101,15 +2101,19 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             const int n_act = __popcll(act);
             const bool alone = n_act == 1 && *wtop == 0;
             if (C.lone && ((n_act <= C.lone_k && *wtop == 0) || C.lone_all)) {
-                const bool hand = active && L.phase == 0;
+                /* a full hand-over queue is read, not claimed, and the photons stay in the lane loop
+                 * (claiming past the cap and skipping the trip would retry forever) */
+                const bool hand = active && L.phase == 0 &&
+                                  __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < C.lone_cap;
                 if (__ballot(hand)) {
                     unsigned long long slot = ~0ull;
                     if (hand) slot = atomicAdd(C.lone_count, 1ull);
-                    if (hand && slot < C.lone_cap) {
+                    const bool handed = hand && slot < C.lone_cap;
+                    if (handed) {
                         export_lone(C.lone + slot, L, cold);
                         active = false;
                     }
-                    continue;
+                    if (__ballot(handed)) continue; /* the rest reach the top of a step on later trips */
                 }
             }
             if (tail && alone) {
@@ -2332,7 +2336,7 @@ struct grm_engine {
     /* photons; -1 = lanes; -2 (default) = auto: lanes for a call of fewer than WARMUP_AUTO_RATIO x lanes
      * photons, else WARMUP_PHOTONS (profiles/r03d_warmup_rank_sweep_1e5.log) */
     int64_t warmup = -2;
-    int warmup_slack = 4;
+    int warmup_slack = -1; /* log2; -1 (default) = auto: 4 when the warm-up ramps to a grid of lanes, else 1 */
     int refill_min = 2;      /* primaries: set-up is in the trip (phase 3), so refill early */
     int child_min = 8;       /* children: batch the divergent scattering sampling */
     uint64_t history = 0;    /* primaries tracked since reset */
@@ -2479,6 +2483,13 @@ int ensure_ovf(grm_engine *e, unsigned long long cap) {
  * A larger call (the bench's photon_n = 1e6: 110 x lanes) keeps WARMUP_PHOTONS: its lag is ~1 % of
  * the pass, and the ramp would cost ~15 % of it. */
 constexpr uint64_t WARMUP_AUTO_RATIO = 32, WARMUP_PHOTONS = 4096;
+/* The barrier before each admission batch waits until in-flight <= history / 2^slack.  With 1/16
+ * (slack 4) the 4,096-photon warm-up of a photon_n = 1e6 pass took ~45 ms of a ~390 ms launch,
+ * waiting on the long-lived families of each batch; with 1/2 (slack 1) ~15 ms, and the pass's
+ * recorded count stayed within the oracle's spread (17.6 / 17.0 M against 17.64 +- 0.55 M;
+ * profiles/r03_ab/r3k_*).  The ramp of small passes (above) keeps 1/16: there the history it builds
+ * is the point. */
+constexpr int WARMUP_SLACK_LARGE = 1;
 
 /* one launch (+ overflow relaunches) over claim positions [pos0, pos1) of a batch of n primaries
  * interleaved as 2^sh runs of m (Ctl.pos_end) */
@@ -2537,13 +2548,14 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
         const uint64_t n_call = pos1 - pos0;
-        const uint64_t limit = e->warmup == -2 ? (n_call < WARMUP_AUTO_RATIO * e->lanes ? (uint64_t)e->lanes : WARMUP_PHOTONS)
+        const bool small = n_call < WARMUP_AUTO_RATIO * e->lanes;
+        const uint64_t limit = e->warmup == -2 ? (small ? (uint64_t)e->lanes : WARMUP_PHOTONS)
                                : e->warmup < 0 ? (uint64_t)e->lanes
                                                : (uint64_t)e->warmup;
         C.admit_n = (!e->bias_mode && e->history < limit && pos0 == 0) ? std::min<uint64_t>(pos1, limit - e->history) : 0;
         C.admit_h0 = e->history;
         C.admit_lim = limit;
-        C.admit_slack = e->warmup_slack;
+        C.admit_slack = e->warmup_slack >= 0 ? e->warmup_slack : (e->warmup == -2 && small ? 4 : WARMUP_SLACK_LARGE);
         C.admit_b0 = e->warmup_b0;
     }
     if (e->bias_mode && e->frozen_set) {
@@ -2933,7 +2945,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_WARMUP: e->warmup = v; return 0;
     case GRM_OPT_REFILL_MIN: e->refill_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_CHILD_MIN: e->child_min = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
-    case GRM_OPT_WARMUP_SLACK: e->warmup_slack = v < 0 ? 0 : (v > 30 ? 30 : (int)v); return 0;
+    case GRM_OPT_WARMUP_SLACK: e->warmup_slack = v < 0 ? -1 : (v > 30 ? 30 : (int)v); return 0;
     case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;

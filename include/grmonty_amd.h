@@ -154,7 +154,9 @@ enum {
     /* scattered children a wavefront samples together (1..64, default 8): larger = less divergent
      * scattering sampling, more idle lane-trips while a batch gathers */
     GRM_OPT_CHILD_MIN = 11,
-    /* warm-up straggler tolerance, log2 (default 4: 1/16 of the history may still be in flight) */
+    /* warm-up straggler tolerance, log2: the next admission batch starts once at most 1/2^slack of
+     * the history is still in flight (default -1 = auto: 4 for the small-pass ramp to a grid of
+     * lanes, 1 for the 4,096-photon warm-up of larger passes) */
     GRM_OPT_WARMUP_SLACK = 12,
     /* 1 (default): a wave whose only work left is one photon hands it to the lone-photon kernel (two
      * waves per photon, after the launch); 0: the lane loop keeps it; 2: every photon is handed over
