@@ -120,6 +120,8 @@ struct Ctl {
     unsigned long long admit_b0; /* first batch */
     unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
+    unsigned long long *phases; /* s_memrealtime when the warm-up admission ended ([0]) and the pool's
+                                 * last claim chunk was taken ([1]); null = not recorded */
     int lanes;
     /* watchdog: a launch older than watchdog_ticks (s_memrealtime, 100 MHz; 0 = off) abandons its
      * photons and exits, so no input can keep the GPU busy without bound.  The first stuck_cap
@@ -1981,7 +1983,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                     const unsigned long long next =
                                         end >= C.admit_n ? ~0ull
                                                          : min(C.admit_n, end + max(C.admit_b0, min(h, C.admit_lim - h)));
-                                    atomicCAS(C.admit_end, end, next);
+                                    if (atomicCAS(C.admit_end, end, next) == end && next == ~0ull && C.phases)
+                                        C.phases[0] = __builtin_amdgcn_s_memrealtime();
                                 }
                             }
                         }
@@ -2004,6 +2007,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                             res_next = b;
                             res_end = min(b + RES_CHUNK, C.pos_end);
                             head_done = b + RES_CHUNK >= C.pos_end;
+                            if (C.phases && lane_id == 0 && b < C.pos_end && head_done)
+                                C.phases[1] = __builtin_amdgcn_s_memrealtime(); /* the one wave of the last chunk */
                         }
                         base = res_next;
                         k_pool = res_end > res_next ? (int)min((unsigned long long)k_pool, res_end - res_next) : 0;
@@ -2600,6 +2605,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
          * [11] workgroups exited, [12] worker running / closed, [13] bulk started */
         const bool early = pass == 0 && C.pool_kind == 0 && e->early_steps > 0 && !C.lone_all && grid > 1;
         if (early) op.set |= 0x3f00u;
+        if (pass == 0 && grid == e->grid) op.set |= (1u << 14) | (1u << 15); /* phase stamps */
         if (ctl(e, op, false)) return -1;
         if (early) {
             C.early_q = e->d_early;
@@ -2620,6 +2626,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.ovf_count = e->d_small + 1 + dst;
         /* the per-wave record is kept of the first launch on the full grid (the bulk of a call) */
         C.waves = (pass == 0 && grid == e->grid) ? e->d_waves : nullptr;
+        C.phases = C.waves ? e->d_small + 14 : nullptr; /* zeroed by the control op above */
         if (C.waves) e->waves_rows = (size_t)grid * (BLOCK / 64);
         if (pass > 0) {
             C.pool = e->d_ovf[src];
@@ -3150,6 +3157,28 @@ int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap) {
     if (k && out && hipMemcpy(out, e->d_waves, k * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return (int64_t)n;
+}
+
+int grm_engine_debug_phases(grm_engine *e, uint64_t out[4]) {
+    if (!e || !out) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    DevCounters h;
+    if (read_counters(e, h)) return -1; /* mirrors the small words */
+    unsigned long long lo = ~0ull, hi = 0;
+    const size_t n = std::min(e->lanes / 64, e->waves_rows);
+    if (n) {
+        std::vector<unsigned long long> w(n * 4);
+        HIPCHK(e, hipMemcpy(w.data(), e->d_waves, n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; ++i) {
+            lo = std::min(lo, w[i * 4]);
+            hi = std::max(hi, w[i * 4 + 1]);
+        }
+    }
+    out[0] = n ? lo : 0;
+    out[1] = e->pin->small[14];
+    out[2] = e->pin->small[15];
+    out[3] = hi;
+    return 0;
 }
 
 int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]) {

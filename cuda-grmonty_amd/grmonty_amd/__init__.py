@@ -144,6 +144,7 @@ SIGNATURES = {
     "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_stuck": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_counters": (C.c_int, [VP, C.POINTER(C.c_uint64)]),
+    "grm_engine_debug_phases": (C.c_int, [VP, C.POINTER(C.c_uint64)]),
     "grm_sizeof": (C.c_size_t, [C.c_int]),
     "grm_version": (C.c_char_p, []),
 }
@@ -405,6 +406,15 @@ class Engine:
         if n < 0:
             raise RuntimeError(self.L.grm_engine_last_error(self.h).decode())
         return out[:n]
+
+    def debug_phases(self) -> dict:
+        """ms from the first wave's start of the last call's main launch to the end of the warm-up
+        admission, to the pool's last claim chunk, and to the last wave's exit"""
+        out = (C.c_uint64 * 4)()
+        self._check(self.L.grm_engine_debug_phases(self.h, out))
+        t0 = out[0]
+        ms = lambda t: (t - t0) * 1e-5 if t else None  # noqa: E731  (100 MHz ticks)
+        return {"warmup_end_ms": ms(out[1]), "pool_drained_ms": ms(out[2]), "last_exit_ms": ms(out[3])}
 
     def debug_counters(self) -> dict:
         """raw device counters (grm_engine_debug_counters)"""

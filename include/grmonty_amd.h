@@ -227,6 +227,10 @@ int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap);
  * n_overflow, n_dropped, n_primaries, max photon steps, lives > 1e5 steps, n_abandoned, abort, n_nan,
  * waves whose kernel-argument check failed, 1 reserved */
 int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]);
+/* diagnostic: the phases of the last call's main launch, s_memrealtime ticks (100 MHz): first wave
+ * start, end of the live-bias warm-up admission (0 = none), the pool's last claim chunk taken (0 =
+ * not reached), last wave exit */
+int grm_engine_debug_phases(grm_engine *e, uint64_t out[4]);
 
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
 /* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */
