@@ -230,12 +230,18 @@ def main():
         # times shorter
         handles = [None] * world
         dist.all_gather_object(handles, engine.counters_ipc_handle())
-        ok = True
-        try:
-            engine.set_peers(handles, rank)
-        except RuntimeError as ex:
-            ok = False
-            print(f"rank {rank}: peer counters unavailable ({ex}); per-rank bias counters", file=sys.stderr)
+        devices = [None] * world
+        dist.all_gather_object(devices, local)
+        # every rank's GPU must be readable from this one (xGMI peer access) before its blocks are mapped
+        ok = all(G.lib().grm_device_peer_ok(local, d) == 1 for d in devices)
+        if ok:
+            try:
+                engine.set_peers(handles, rank)
+            except RuntimeError as ex:
+                ok = False
+                print(f"rank {rank}: peer counters unavailable ({ex}); per-rank bias counters", file=sys.stderr)
+        else:
+            print(f"rank {rank}: no peer access to every rank's GPU; per-rank bias counters", file=sys.stderr)
         flags = [None] * world
         dist.all_gather_object(flags, ok)
         if not all(flags):

@@ -649,7 +649,8 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const double x[4], co
  * 2 x 11 x 8 B x 512 lanes = 88 KB (+ 40 KB of lane fields, 16 KB of lane ints): no global memory
  * traffic on the halving path. */
 constexpr int LDS_DOUBLES_PER_LANE = 11;
-constexpr unsigned WARM_BLOCKS = 64; /* workgroups that take the warm-up's admission batches */
+constexpr unsigned WARM_BLOCKS = 64;
+constexpr unsigned PHASE_LOG = 64; /* words of the launch's phase log (after the per-wave record) */ /* workgroups that take the warm-up's admission batches */
 constexpr unsigned long long RES_CHUNK = 64; /* claim positions a wave reserves per pool-head atomic */
 
 __device__ __forceinline__ void save_xkdk(const Slot &s, const Lane &L) {
@@ -1983,8 +1984,18 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                     const unsigned long long next =
                                         end >= C.admit_n ? ~0ull
                                                          : min(C.admit_n, end + max(C.admit_b0, min(h, C.admit_lim - h)));
-                                    if (atomicCAS(C.admit_end, end, next) == end && next == ~0ull && C.phases)
-                                        C.phases[0] = __builtin_amdgcn_s_memrealtime();
+                                    if (atomicCAS(C.admit_end, end, next) == end && C.phases) {
+                                        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                                        if (next == ~0ull) C.phases[0] = t;
+                                        /* the admission log: [3 + 2k] when batch k + 1 opened, [4 + 2k]
+                                         * the photons then in flight */
+                                        const unsigned long long k = atomicAdd(C.phases + 2, 1ull);
+                                        if (k < (PHASE_LOG - 3) / 2) {
+                                            C.phases[3 + 2 * k] = t;
+                                            C.phases[4 + 2 * k] = __hip_atomic_load(C.in_flight, __ATOMIC_RELAXED,
+                                                                                    __HIP_MEMORY_SCOPE_AGENT);
+                                        }
+                                    }
                                 }
                             }
                         }
@@ -2451,7 +2462,8 @@ int alloc_lanes(grm_engine *e) {
         HIPCHK(e, hipMalloc(&e->d_cold, lanes * sizeof(Cold)));
         if (e->d_waves) (void)hipFree(e->d_waves);
         e->d_waves = nullptr;
-        HIPCHK(e, hipMalloc(&e->d_waves, lanes / 64 * 4 * sizeof(unsigned long long)));
+        /* + PHASE_LOG words: the launch's phase stamps (grm_engine_debug_phases / _admissions) */
+        HIPCHK(e, hipMalloc(&e->d_waves, (lanes / 64 * 4 + PHASE_LOG) * sizeof(unsigned long long)));
         if (e->d_spec_blocks) (void)hipFree(e->d_spec_blocks);
         e->d_spec_blocks = nullptr;
         HIPCHK(e, hipMalloc(&e->d_spec_blocks, (size_t)grid * SPEC_LDS * sizeof(double)));
@@ -2605,7 +2617,6 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
          * [11] workgroups exited, [12] worker running / closed, [13] bulk started */
         const bool early = pass == 0 && C.pool_kind == 0 && e->early_steps > 0 && !C.lone_all && grid > 1;
         if (early) op.set |= 0x3f00u;
-        if (pass == 0 && grid == e->grid) op.set |= (1u << 14) | (1u << 15); /* phase stamps */
         if (ctl(e, op, false)) return -1;
         if (early) {
             C.early_q = e->d_early;
@@ -2626,7 +2637,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.ovf_count = e->d_small + 1 + dst;
         /* the per-wave record is kept of the first launch on the full grid (the bulk of a call) */
         C.waves = (pass == 0 && grid == e->grid) ? e->d_waves : nullptr;
-        C.phases = C.waves ? e->d_small + 14 : nullptr; /* zeroed by the control op above */
+        C.phases = C.waves ? e->d_waves + (size_t)(e->lanes / 64) * 4 : nullptr;
+        if (C.phases) HIPCHK(e, hipMemsetAsync(C.phases, 0, PHASE_LOG * sizeof(unsigned long long), e->stream));
         if (C.waves) e->waves_rows = (size_t)grid * (BLOCK / 64);
         if (pass > 0) {
             C.pool = e->d_ovf[src];
@@ -3174,11 +3186,26 @@ int grm_engine_debug_phases(grm_engine *e, uint64_t out[4]) {
             hi = std::max(hi, w[i * 4 + 1]);
         }
     }
+    unsigned long long ph[2] = {0, 0};
+    if (n) HIPCHK(e, hipMemcpy(ph, e->d_waves + (e->lanes / 64) * 4, sizeof(ph), hipMemcpyDeviceToHost));
     out[0] = n ? lo : 0;
-    out[1] = e->pin->small[14];
-    out[2] = e->pin->small[15];
+    out[1] = ph[0];
+    out[2] = ph[1];
     out[3] = hi;
     return 0;
+}
+
+int64_t grm_engine_debug_admissions(grm_engine *e, uint64_t *out, size_t cap) {
+    if (!e || !e->d_waves || !e->waves_rows) return -1;
+    HIPCHK(e, hipSetDevice(e->device));
+    unsigned long long ph[PHASE_LOG];
+    HIPCHK(e, hipMemcpy(ph, e->d_waves + (e->lanes / 64) * 4, sizeof(ph), hipMemcpyDeviceToHost));
+    const size_t k = std::min<size_t>(ph[2], (PHASE_LOG - 3) / 2);
+    for (size_t i = 0; i < k && i < cap; ++i) {
+        out[2 * i] = ph[3 + 2 * i];
+        out[2 * i + 1] = ph[4 + 2 * i];
+    }
+    return (int64_t)k;
 }
 
 int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]) {
@@ -3358,6 +3385,13 @@ int grm_engine_set_peers(grm_engine *e, const uint8_t *handles, int n, int rank)
         }
     }
     return upload_peers(e, tab);
+}
+
+int grm_device_peer_ok(int device, int peer) {
+    if (device == peer) return 1;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess) return 0;
+    return can ? 1 : 0;
 }
 
 int grm_engine_link_peers(grm_engine *const *engines, int n) {

@@ -140,11 +140,13 @@ SIGNATURES = {
     "grm_engine_set_peers": (C.c_int, [VP, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     "grm_engine_link_peers": (C.c_int, [C.POINTER(VP), C.c_int]),
     "grm_engine_job_counters": (C.c_int, [VP, DP]),
+    "grm_device_peer_ok": (C.c_int, [C.c_int, C.c_int]),
     "grm_engine_debug_timing": (C.c_int, [VP, C.POINTER(C.c_uint64), C.c_int]),
     "grm_engine_debug_waves": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_stuck": (C.c_int64, [VP, VP, C.c_size_t]),
     "grm_engine_debug_counters": (C.c_int, [VP, C.POINTER(C.c_uint64)]),
     "grm_engine_debug_phases": (C.c_int, [VP, C.POINTER(C.c_uint64)]),
+    "grm_engine_debug_admissions": (C.c_int64, [VP, C.POINTER(C.c_uint64), C.c_size_t]),
     "grm_sizeof": (C.c_size_t, [C.c_int]),
     "grm_version": (C.c_char_p, []),
 }
@@ -414,7 +416,11 @@ class Engine:
         self._check(self.L.grm_engine_debug_phases(self.h, out))
         t0 = out[0]
         ms = lambda t: (t - t0) * 1e-5 if t else None  # noqa: E731  (100 MHz ticks)
-        return {"warmup_end_ms": ms(out[1]), "pool_drained_ms": ms(out[2]), "last_exit_ms": ms(out[3])}
+        adm = (C.c_uint64 * 64)()
+        k = self.L.grm_engine_debug_admissions(self.h, adm, 32)
+        batches = [(ms(adm[2 * i]), int(adm[2 * i + 1])) for i in range(max(0, min(k, 32)))]
+        return {"warmup_end_ms": ms(out[1]), "pool_drained_ms": ms(out[2]), "last_exit_ms": ms(out[3]),
+                "admissions": batches}
 
     def debug_counters(self) -> dict:
         """raw device counters (grm_engine_debug_counters)"""

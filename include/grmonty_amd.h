@@ -231,6 +231,9 @@ int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]);
  * start, end of the live-bias warm-up admission (0 = none), the pool's last claim chunk taken (0 =
  * not reached), last wave exit */
 int grm_engine_debug_phases(grm_engine *e, uint64_t out[4]);
+/* the live-bias warm-up's admission log of the same launch: out[2i] = s_memrealtime tick when batch
+ * i + 1 opened, out[2i + 1] = photons in flight then (i < cap); returns the number of openings */
+int64_t grm_engine_debug_admissions(grm_engine *e, uint64_t *out, size_t cap);
 
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
 /* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */
@@ -279,6 +282,9 @@ int grm_engine_counters_ipc_handle(grm_engine *e, uint8_t out[64]);
 int grm_engine_set_peers(grm_engine *e, const uint8_t *handles, int n, int rank);
 int grm_engine_link_peers(grm_engine *const *engines, int n);
 int grm_engine_job_counters(grm_engine *e, double out[4]);
+/* 1 if device `device` can read device `peer`'s memory (hipDeviceCanAccessPeer; same device: 1) --
+ * checked by bench.py for every rank's GPU before grm_engine_set_peers */
+int grm_device_peer_ok(int device, int peer);
 
 /* --- host model (harm_model.hpp; C++ host, no GPU) ------------------------------------- */
 typedef struct grm_model grm_model;

@@ -32,3 +32,4 @@ for s in range(n):
           f"{ph['warmup_end_ms']:.1f} ms, pool drained {ph['pool_drained_ms']:.1f} ms, wave exits p10/50/90/100 "
           f"{ex[len(ex) // 10]:.1f}/{ex[len(ex) // 2]:.1f}/{ex[9 * len(ex) // 10]:.1f}/{ex[-1]:.1f} ms; lone "
           f"{st['n_lone']} photons {st['lone_ms']:.1f} ms, launches {st['n_launches']}", flush=True)
+    print("   admissions (ms, in flight): " + " ".join(f"{t:.1f}/{f}" for t, f in ph["admissions"]), flush=True)

@@ -1,10 +1,8 @@
 #!/bin/bash
-# one laundered kernarg pointer for Params and Ctl (one) vs two (pc); lone-kernel laundering (onel)
-# on the deterministic lone-latency probe
+# Round-3 session m: timeline of the main launch (warm-up end, pool drained, last exit), 1e6 and 1e7
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R" && mkdir -p gpurun_out
-for v in one onel pc; do
-  GRMONTY_AMD_LIB="$R/cuda-grmonty_amd/variants/libgrmonty_amd_v$v.so" timeout -k 10 200 python tools/lone_bench.py 512 3 > gpurun_out/r3m_lone_$v.log 2>&1 || { tail -5 gpurun_out/r3m_lone_$v.log; exit 1; }
-  echo "$v $(grep rep gpurun_out/r3m_lone_$v.log | tail -2 | cut -c1-150)"
-done
-VARIANTS="one pc" ROUNDS=2 STEPS=6 TAG=r3m bash tools/ab_bench.sh || exit 1
+timeout -k 10 300 python -u tools/pass_phases.py 5 1e6 > gpurun_out/r3m_phases_1e6.log 2>&1 || { tail -5 gpurun_out/r3m_phases_1e6.log; exit 1; }
+cat gpurun_out/r3m_phases_1e6.log
+timeout -k 10 300 python -u tools/pass_phases.py 2 1e7 > gpurun_out/r3m_phases_1e7.log 2>&1 || { tail -5 gpurun_out/r3m_phases_1e7.log; exit 1; }
+cat gpurun_out/r3m_phases_1e7.log
 rm -f gpurun_out/*.dump
