@@ -31,5 +31,6 @@ for s in range(n):
     print(f"seed {123 + s}: dominant {st['max_launch_ms']:.1f} ms, steps {st['max_launch_steps']:.4g}; warm-up ends "
           f"{ph['warmup_end_ms']:.1f} ms, pool drained {ph['pool_drained_ms']:.1f} ms, wave exits p10/50/90/100 "
           f"{ex[len(ex) // 10]:.1f}/{ex[len(ex) // 2]:.1f}/{ex[9 * len(ex) // 10]:.1f}/{ex[-1]:.1f} ms; lone "
-          f"{st['n_lone']} photons {st['lone_ms']:.1f} ms, launches {st['n_launches']}", flush=True)
+          f"{st['n_lone']} photons {st['lone_ms']:.1f} ms, launches {st['n_launches']}; recorded {e.debug_counters()['n_recorded']} "
+          f"dropped {st['n_dropped']} abandoned {st['n_abandoned']}", flush=True)
     print("   admissions (ms, in flight): " + " ".join(f"{t:.1f}/{f}" for t, f in ph["admissions"]), flush=True)
