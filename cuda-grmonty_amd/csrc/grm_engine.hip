@@ -119,13 +119,6 @@ struct Ctl {
     int admit_slack;
     unsigned long long admit_b0; /* first batch */
     unsigned long long admit_spread; /* photons one wave claims at most per warm-up claim (0: no cap) */
-    /* the warm-up's shared child queue (GRM_OPT_WARMUP_SHARE; null: off): while the admission is in
-     * force a child goes here instead of its wave's stack, and any wave of the warm-up takes it, so
-     * one primary's family (the first photons' bias is large: hundreds of scatterings) spreads over
-     * the warm-up's waves.  share[slot] is valid once share_ready[slot] == share_tag */
-    SReq *share;
-    unsigned long long *share_ready, *share_tail, *share_head;
-    unsigned long long share_cap, share_tag;
     unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     unsigned long long *phases; /* s_memrealtime when the warm-up admission ended ([0]) and the pool's
@@ -632,23 +625,13 @@ __device__ __forceinline__ void push_overflow_req(const Ctl &C, const SReq &R) {
     atomicAdd(&C.ctr->n_overflow, 1ull);
 }
 
-/* push the scattered photon's child out as a scatter request: during the warm-up with `share`,
- * onto the warm-up's shared queue; else onto the wave's stack (HBM entries, top counter in LDS); a
- * full one: the overflow pool (tracked by the next launch).  true = on the queue or the stack */
+/* push the scattered photon's child out as a scatter request: onto the wave's stack (HBM entries,
+ * top counter in LDS), else the overflow pool (tracked by the next launch).  true = on the stack */
 __device__ __forceinline__ bool push_request(const Ctl &C, const double x[4], const double k[4], const Rng &rng,
                                              int n_scatt, const Cold *cold, const Fluid &F, double wc, SReq *wstack,
-                                             int *wtop, bool share) {
+                                             int *wtop) {
     SReq R;
     make_sreq(R, x, k, rng, n_scatt, cold, F, wc);
-    if (share) { /* the warm-up's shared queue; full: the wave's stack as below */
-        const unsigned long long q = atomicAdd(C.share_tail, 1ull);
-        if (q < C.share_cap) {
-            store_sreq(C.share + q, R);
-            __threadfence();
-            __hip_atomic_store(C.share_ready + q, C.share_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            return true;
-        }
-    }
     const int slot = atomicAdd(wtop, 1); /* LDS; values past the cap are clamped at the next refill */
     if (slot < WSTACK_CAP) {
         store_sreq(wstack + slot, R);
@@ -1643,7 +1626,7 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
  * whole wave waiting for the deepest halving tree.  `walked`: halving_walk has just completed this
  * lane's push (its phase-0 block ran before it).  Returns false when the photon's life ended. */
 __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *wstack, int *wtop,
-                               const Slot &ph2, const Slot &bk, double bias_d, bool walked, bool share) {
+                               const Slot &ph2, const Slot &bk, double bias_d, bool walked) {
     if (L.phase == 0 && !trip_begin(P, C, L, cold, ph2)) return false;
     TSTAMP(8);
     /* one attempt of push_photon at the current node of the halving tree (:1217-1289).  A lane in
@@ -1750,7 +1733,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             /* the child leaves as a scatter request; its stores go out after this trip's table
              * loads, so no load of the trip waits behind them (vmcnt is in order) */
             if (F.n_e > 0.0) {
-                if (push_request(C, L.x, L.k, L.rng, L.n_scatt(), cold, F, L.p_wc(), wstack, wtop, share)) ++L.flight();
+                if (push_request(C, L.x, L.k, L.rng, L.n_scatt(), cold, F, L.p_wc(), wstack, wtop)) ++L.flight();
                 ++L.c_children();
             }
             L.alpha_scatti() = a_s;
@@ -1884,10 +1867,6 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     unsigned long long res_next = 0, res_end = 0; /* wave-uniform: reserved claim positions */
     bool head_done = false;      /* wave-uniform: the pool head has passed pos_end */
     bool warm = !karg_bad && C0.admit_n != 0; /* wave-uniform: warm-up admission in force */
-    /* wave-uniform: this wave takes children from the warm-up's shared queue (until it has seen the
-     * queue empty after its warm-up, or at its exit; a wave that pushed there checks it before it
-     * leaves, so no child stays behind) */
-    bool share_live = warm && C0.share != nullptr && blockIdx.x < WARM_BLOCKS;
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
     L.flight() = 0;
     /* wave-uniform; refreshed every trip during the warm-up and every REFRESH_TRIPS trips after it
@@ -1960,8 +1939,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             const int n_idle = __popcll(idle);
             const bool none_active = idle == __ballot(1);
             const bool child_due = top >= C.child_min || (pool_done && top > 0);
-            int k_child = 0, k_pool = 0, k_share = 0;
-            unsigned long long sbase = 0;
+            int k_child = 0, k_pool = 0;
             bool go;
             if (none_active || child_due) {
                 k_child = n_idle < top ? n_idle : top;
@@ -1971,36 +1949,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 k_pool = pool_done ? 0 : n_idle;
                 go = k_pool >= C.refill_min;
             }
-            if (share_live && n_idle > k_child) {
-                /* children of the shared queue before primaries (the stack's children first) */
-                long long got = 0;
-                int empty = 0;
-                if (lane_id == 0) {
-                    const unsigned long long tl =
-                        __hip_atomic_load(C.share_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned long long hd =
-                        __hip_atomic_load(C.share_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned long long lim = min(tl, C.share_cap);
-                    if (hd < lim) {
-                        const unsigned long long want = min((unsigned long long)(n_idle - k_child), lim - hd);
-                        if (atomicCAS(C.share_head, hd, hd + want) == hd) {
-                            got = (long long)want;
-                            sbase = hd;
-                        }
-                    } else {
-                        empty = 1;
-                    }
-                }
-                k_share = (int)__shfl(got, 0);
-                sbase = __shfl(sbase, 0);
-                if (__shfl(empty, 0) && (!warm || (pool_done && !__any(active) && *wtop == 0))) share_live = false;
-                if (k_share > 0) {
-                    go = true;
-                    k_pool = min(k_pool, n_idle - k_child - k_share);
-                }
-            }
             if (go) {
-                const int r = __popcll(idle & lt_mask) - k_share; /* share lanes first: r < 0 */
+                const int r = __popcll(idle & lt_mask);
                 unsigned long long base = 0;
                 if (k_pool > 0) {
                     if (warm) {
@@ -2084,28 +2034,12 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
 #endif
                 TSTAMP(14);
                 bool has = false, ok = true;
-                if (!active && r >= 0 && r < k_child) {
+                if (!active && r < k_child) {
                     SReq R;
                     load_sreq(wstack + (top - 1 - r), R);
                     ok = sample_child(P, C, R, L, cold);
                     if (!ok && C.trace)
                         write_trace(C, cold, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4, -1, -1);
-                    has = true;
-                }
-                if (!active && r < 0) { /* a child of the shared queue: -k_share <= r < 0 */
-                    const unsigned long long q = sbase + (unsigned long long)(r + k_share);
-                    unsigned spin = 0;
-                    while (__hip_atomic_load(C.share_ready + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.share_tag &&
-                           ++spin < (1u << 20))
-                        __builtin_amdgcn_s_sleep(1);
-                    if (spin < (1u << 20)) {
-                        SReq R;
-                        load_sreq(C.share + q, R);
-                        ok = sample_child(P, C, R, L, cold);
-                    } else { /* its producer never published it (cannot happen short of a bug) */
-                        atomicAdd(&C.ctr->n_dropped, 1ull);
-                        ok = false;
-                    }
                     has = true;
                 }
                 TSTAMP(0);
@@ -2145,7 +2079,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 if (lane_id == 0 && d) atomicAdd(C.in_flight, (unsigned long long)(long long)d);
                 L.flight() = 0;
             }
-            if (pool_done && *wtop == 0 && !share_live) break;
+            if (pool_done && *wtop == 0) break;
             if (warm) {
                 /* waiting for the next batch; a barrier that never opens (it cannot, short of a
                  * counting bug) must not hang the GPU: after ~1 s give the warm-up up for all */
@@ -2214,7 +2148,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             }
         }
         if (active) {
-            active = !ended && transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked, warm && C.share);
+            active = !ended && transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked);
             if (!active) {
                 L.c_nstep_max() = max((int)L.c_nstep_max(), L.n_step);
                 L.c_long() += L.n_step > 100000 ? 1 : 0;
@@ -2453,11 +2387,14 @@ struct grm_engine {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_pre = nullptr, ev_w = nullptr;
     unsigned long long warmup_b0 = 64;     /* GRM_OPT_WARMUP_BATCH */
-    unsigned long long warmup_spread = 0;  /* GRM_OPT_WARMUP_SPREAD */
-    int warmup_share = 0;                  /* GRM_OPT_WARMUP_SHARE */
-    static constexpr unsigned long long SHARE_CAP = 1ull << 17; /* the warm-up's shared child queue */
-    SReq *d_share = nullptr;
-    unsigned long long *d_share_ready = nullptr;
+    /* GRM_OPT_WARMUP_SPREAD: 4 photons per wave claim spread a batch over 4-16x more waves, so the
+     * families of its photons (the first photons' bias is large: long scattering cascades, each on
+     * its wave's stack) get more lanes each -- the warm-up of a photon_n = 1e6 pass ends at ~28 ms
+     * instead of ~49, recorded unchanged within 1.3 % (12 passes per setting, profiles/r03_ab/
+     * r03p_warmup_spread_*.log; 1: 41 ms, 2: 32, 8: 29, 16: 31).  -1 (default) = auto: 4 for the
+     * WARMUP_PHOTONS warm-up; none for the ramp to a grid of lanes (its batches outnumber the
+     * warm-up's lanes) */
+    int64_t warmup_spread = -1;
     /* host-mapped control block: ctl_kernel mirrors the counters and the small words here (ctr,
      * small) and the emission scan writes its total (word[4]); the host reads them after a stream
      * synchronisation, so a pass runs without copy or fill kernels (see ctl_kernel) */
@@ -2571,13 +2508,16 @@ int ensure_ovf(grm_engine *e, unsigned long long cap) {
  * A larger call (the bench's photon_n = 1e6: 110 x lanes) keeps WARMUP_PHOTONS: its lag is ~1 % of
  * the pass, and the ramp would cost ~15 % of it. */
 constexpr uint64_t WARMUP_AUTO_RATIO = 32, WARMUP_PHOTONS = 4096;
-/* The barrier before each admission batch waits until in-flight <= history / 2^slack.  With 1/16
- * (slack 4) the 4,096-photon warm-up of a photon_n = 1e6 pass took ~45 ms of a ~390 ms launch,
- * waiting on the long-lived families of each batch; with 1/2 (slack 1) ~15 ms, and the pass's
- * recorded count stayed within the oracle's spread (17.6 / 17.0 M against 17.64 +- 0.55 M;
- * profiles/r03_ab/r3k_*).  The ramp of small passes (above) keeps 1/16: there the history it builds
- * is the point. */
+/* The barrier before each admission batch waits until in-flight <= history / 2^slack.  Slack 1
+ * (1/2) instead of 4 (1/16) shortened a photon_n = 1e6 launch by ~30 ms, the recorded count within
+ * the oracle's spread (17.6 / 17.0 M against 17.64 +- 0.55 M; profiles/r03_ab/r3k_*).  The
+ * admission log (grm_engine_debug_admissions, profiles/r03_ab/r03o_*) then shows batches 2-7
+ * opening within 0.3 ms and the end of the warm-up at ~48 ms: the last batch waits for the
+ * scattering families of its photons (the first photons' bias is large), each on its own wave's
+ * stack -- hence WARMUP_SPREAD photons per wave claim (~28 ms).  The ramp of small passes (above)
+ * keeps 1/16: there the history it builds is the point. */
 constexpr int WARMUP_SLACK_LARGE = 1;
+constexpr unsigned long long WARMUP_SPREAD = 4;
 
 /* one launch (+ overflow relaunches) over claim positions [pos0, pos1) of a batch of n primaries
  * interleaved as 2^sh runs of m (Ctl.pos_end) */
@@ -2645,7 +2585,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.admit_lim = limit;
         C.admit_slack = e->warmup_slack >= 0 ? e->warmup_slack : (e->warmup == -2 && small ? 4 : WARMUP_SLACK_LARGE);
         C.admit_b0 = e->warmup_b0;
-        C.admit_spread = e->warmup_spread;
+        C.admit_spread = e->warmup_spread >= 0 ? (unsigned long long)e->warmup_spread
+                                               : (e->warmup == -2 && small ? 0ull : WARMUP_SPREAD);
     }
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
@@ -2689,18 +2630,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
          * [11] workgroups exited, [12] worker running / closed, [13] bulk started */
         const bool early = pass == 0 && C.pool_kind == 0 && e->early_steps > 0 && !C.lone_all && grid > 1;
         if (early) op.set |= 0x3f00u;
-        /* the warm-up's shared child queue: [14] tail, [15] head */
-        const bool share = pass == 0 && C.admit_n && e->warmup_share && e->d_share;
-        if (share) op.set |= (1u << 14) | (1u << 15);
         if (ctl(e, op, false)) return -1;
-        C.share = share ? e->d_share : nullptr;
-        if (share) {
-            C.share_ready = e->d_share_ready;
-            C.share_tail = e->d_small + 14;
-            C.share_head = e->d_small + 15;
-            C.share_cap = grm_engine::SHARE_CAP;
-            C.share_tag = ++e->launch_seq;
-        }
         if (early) {
             C.early_q = e->d_early;
             C.early_ready = e->d_early_ready;
@@ -3018,22 +2948,11 @@ void grm_engine_destroy(grm_engine *e) {
     if (e->stream2) hipStreamDestroy(e->stream2);
     hipFree(e->d_early);
     hipFree(e->d_early_ready);
-    hipFree(e->d_share);
-    hipFree(e->d_share_ready);
     if (e->stream) hipStreamDestroy(e->stream);
     delete e;
 }
 
 const char *grm_engine_last_error(const grm_engine *e) { return e ? e->err.c_str() : "null engine"; }
-
-/* the warm-up's shared child queue, allocated once (ready tags start at zero; tags are never 0) */
-static int share_alloc(grm_engine *e) {
-    if (e->d_share) return 0;
-    HIPCHK(e, hipMalloc(&e->d_share, grm_engine::SHARE_CAP * sizeof(SReq)));
-    HIPCHK(e, hipMalloc(&e->d_share_ready, grm_engine::SHARE_CAP * sizeof(unsigned long long)));
-    HIPCHK(e, hipMemset(e->d_share_ready, 0, grm_engine::SHARE_CAP * sizeof(unsigned long long)));
-    return 0;
-}
 
 int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     if (!e) return -1;
@@ -3061,10 +2980,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_WARMUP_SLACK: e->warmup_slack = v < 0 ? -1 : (v > 30 ? 30 : (int)v); return 0;
     case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
-    case GRM_OPT_WARMUP_SPREAD: e->warmup_spread = v < 0 ? 0 : (unsigned long long)v; return 0;
-    case GRM_OPT_WARMUP_SHARE:
-        e->warmup_share = v ? 1 : 0;
-        return e->warmup_share ? share_alloc(e) : 0;
+    case GRM_OPT_WARMUP_SPREAD: e->warmup_spread = v < 0 ? -1 : v; return 0;
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;

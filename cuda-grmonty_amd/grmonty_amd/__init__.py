@@ -55,7 +55,6 @@ OPT_EARLY_SERIAL = 16
 OPT_KARG_TEST = 17
 OPT_LONE_K = 18
 OPT_WARMUP_SPREAD = 19
-OPT_WARMUP_SHARE = 20
 N_TH_BINS, N_E_BINS = 6, 200
 
 

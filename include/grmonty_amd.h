@@ -178,12 +178,10 @@ enum {
      * most this many photons (1..64, default 1) hands them all to two-wave pairs of the lone kernel
      * instead of stepping them in a nearly empty lane loop */
     GRM_OPT_LONE_K = 18,
-    /* a wave claims at most this many photons of a warm-up admission batch at a time (default 0: as
-     * many lanes as it has idle), spreading the batch over more waves */
-    GRM_OPT_WARMUP_SPREAD = 19,
-    /* 1: during the warm-up admission a scattered photon's child goes to a queue shared by the
-     * warm-up's waves instead of its own wave's stack (0: the stack) */
-    GRM_OPT_WARMUP_SHARE = 20
+    /* a wave claims at most this many photons of a warm-up admission batch at a time, spreading the
+     * batch, and its photons' scattering families, over more waves (0: as many lanes as it has idle;
+     * -1, the default: 4 in the 4,096-photon warm-up, 0 in the ramp of a small pass) */
+    GRM_OPT_WARMUP_SPREAD = 19
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

@@ -1,7 +1,10 @@
 #!/bin/bash
-# dynamic VALU breakdown of track_kernel (what the 20 non-fp64 VALU instructions per step are)
+# Round-3 session p: warm-up spread sweep (GRM_OPT_WARMUP_SPREAD = 19) at photon_n = 1e6, 12 passes each:
+# warm-up end time, dominant launch and recorded per pass
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R" && mkdir -p gpurun_out
-PMC_SETS="SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32;SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_INSTS_SALU;SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU" \
-  PROF_TAG=r02r DIAG="192 1e6" bash tools/gpu_pmc.sh > gpurun_out/r02r_pmc_breakdown.txt 2>&1 || exit 1
-tail -40 gpurun_out/r02r_pmc_breakdown.txt
+for v in "" "19=1" "19=2" "19=4" "19=8" "19=16"; do
+  t="${v:-default}"; t="${t//=/_}"
+  GRM_BENCH_OPTS="$v" timeout -k 10 200 python -u tools/pass_phases.py 12 1e6 > gpurun_out/r3p_spread_$t.log 2>&1 || { tail -5 gpurun_out/r3p_spread_$t.log; exit 1; }
+  echo "== $t"; grep -v admissions gpurun_out/r3p_spread_$t.log
+done
 rm -f gpurun_out/*.dump
