@@ -549,6 +549,107 @@ __device__ __forceinline__ bool push_attempt(const Params &P, double x[4], doubl
     return push_finish(C, k, kp, dk, dl, e_0_s, G.g00, G.g01, G.g03, e_1);
 }
 
+/* ---- quad-parallel push (one photon per quad of lanes: the serial chain of a lone photon) ----
+ * A single wave issues a wave-instruction every ~4.4 cycles whether 1 or 64 lanes are active, so a
+ * push that every lane makes identically pays the full instruction count.  Here the four lanes of a
+ * quad hold the same attempt and lane q = lane & 3 owns row q of the connection: the rows are formed
+ * in four exec-masked blocks (the same instructions as one lane forming all four), and the corrector
+ * -- two passes of four row contractions and four tolerance ratios, ~40 % of an attempt -- runs ONE
+ * row per lane on a uniform instruction stream; k and the ratios are exchanged inside the quad by
+ * DPP quad_perm moves (no LDS, no SGPR round trip).  Each row is contracted with the reference's own
+ * expression and the ratios are summed in its order (e_0 + e_1) + e_2 + e_3, so every lane ends with
+ * the bits of push_attempt. */
+template <int I>
+__device__ __forceinline__ double quad_bcast(double v) {
+    constexpr int ctl = I | (I << 2) | (I << 4) | (I << 6); /* quad_perm [I, I, I, I] */
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, ctl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), ctl, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+/* v[q] for the lane's quad position q (three selects per 32-bit half) */
+__device__ __forceinline__ double quad_pick(const double v[4], int q) {
+    const double lo = (q & 1) ? v[1] : v[0], hi = (q & 1) ? v[3] : v[2];
+    return (q & 2) ? hi : lo;
+}
+
+/* row q of the connection (harm_model.cpp:1436-1569) into L, from the shared products */
+__device__ __forceinline__ void connection_quad_row(const Params &P, const Trig &T, int q, double L[10]) {
+    ConnPre Q;
+    connection_pre(P, T, Q);
+    if (q == 0)
+        connection_row(Q, 0, L);
+    else if (q == 1)
+        connection_row(Q, 1, L);
+    else if (q == 2)
+        connection_row(Q, 2, L);
+    else
+        connection_row(Q, 3, L);
+}
+
+/* geo_rhs of one row (the same expression, harm_model.cpp:1255-1262) */
+__device__ __forceinline__ double geo_rhs_row(const double L[10], const double k[4]) {
+    double d = -2.0 * (k[0] * (L[1] * k[1] + L[2] * k[2] + L[3] * k[3]) + k[1] * (L[5] * k[2] + L[6] * k[3]) +
+                       L[8] * k[2] * k[3]);
+    d -= (L[0] * k[0] * k[0] + L[4] * k[1] * k[1] + L[7] * k[2] * k[2] + L[9] * k[3] * k[3]);
+    return d;
+}
+
+/* row q by selection from all four rows formed on every lane (full ILP, 60 selects) */
+__device__ __forceinline__ void connection_quad_sel(const Params &P, const Trig &T, int q, double L[10]) {
+    Conn C;
+    connection(P, T, C);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        const double v[4] = {C.c[0][j], C.c[1][j], C.c[2][j], C.c[3][j]};
+        L[j] = quad_pick(v, q);
+    }
+}
+
+/* push_attempt on a quad (q = lane & 3; x, k, dk, e_0_s identical over the quad on entry and exit) */
+template <int ROWS = 0>
+__device__ __forceinline__ bool push_attempt_quad(const Params &P, double x[4], double k[4], double dk[4],
+                                                  double e_0_s, double dl, double &e_1, Trig &T, Gcov &G, int q) {
+    double kp[4];
+    push_kick(x, k, dk, dl, kp);
+    trig_at(P, x, T);
+    double L[10];
+    if (ROWS == 0)
+        connection_quad_row(P, T, q, L);
+    else
+        connection_quad_sel(P, T, q, L);
+    gcov_from_trig(P, T, G);
+    const double dl_2 = 0.5 * dl;
+    const double kq = quad_pick(k, q); /* the half-kicked k^q */
+    double kcq = quad_pick(kp, q);     /* k_cont^q */
+    double kc[4] = {kp[0], kp[1], kp[2], kp[3]};
+    double err, dkq;
+    int iter = 0;
+    do {
+        ++iter;
+        dkq = geo_rhs_row(L, kc);
+        const double kpq = kq + dl_2 * dkq;
+        const double eq = fratio_tol(kcq - kpq, kpq + EPS);
+        err = ((0.0 + quad_bcast<0>(eq)) + quad_bcast<1>(eq)) + quad_bcast<2>(eq);
+        err += quad_bcast<3>(eq);
+        kc[0] = quad_bcast<0>(kpq);
+        kc[1] = quad_bcast<1>(kpq);
+        kc[2] = quad_bcast<2>(kpq);
+        kc[3] = quad_bcast<3>(kpq);
+        kcq = kpq;
+    } while (err > E_TOL && iter < MAX_ITER);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k[i] = kc[i];
+    dk[0] = quad_bcast<0>(dkq);
+    dk[1] = quad_bcast<1>(dkq);
+    dk[2] = quad_bcast<2>(dkq);
+    dk[3] = quad_bcast<3>(dkq);
+    e_1 = -(k[0] * G.g00 + k[1] * G.g01 + k[3] * G.g03);
+    const bool err_e = fabs(e_1 - e_0_s) > 1.0e-4 * fabs(e_0_s);
+    return (err_e || err > E_TOL || isnan(err) || isinf(err));
+}
+
 /* Per-lane spill slot for the push backup, laid out [component][lane] so that a wave's
  * accesses are consecutive 8-B words (conflict-free ds_read_b64 / ds_write_b64).  The
  * transport kernel points it at LDS; the probe kernel at a private array. */

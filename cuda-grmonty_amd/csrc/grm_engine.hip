@@ -962,9 +962,25 @@ __device__ __forceinline__ bool kargs_check(KArgsK *ka, const Params &P, const C
     return __builtin_amdgcn_readfirstlane((int)ok) != 0;
 }
 
+/* The push's uniform inputs for the geometry wave's loop, held in VGPRs.  The lone kernels take
+ * (Params, Ctl) by value; the ~0.7 KB of arguments do not fit the SGPR file next to the interaction
+ * wave's code, so the compiler spills them into lanes of a VGPR and reloads each use with a
+ * v_readlane (a VALU instruction, plus hazard nops before the SGPR is read): 1,118 such reloads in
+ * lone_kernel, dozens of them inside one push.  Copies made lane-varying by an empty asm live in
+ * VGPR pairs instead (26 VGPRs of the 512 a single wave per SIMD has) and feed the fp64 VALU
+ * directly.  Same values, same operations. */
+__device__ __forceinline__ void push_params_vgpr(Params &G) {
+#ifndef GRM_X_NO_GEO_VGPR
+    asm volatile("" : "+v"(G.a), "+v"(G.a2), "+v"(G.a3), "+v"(G.a4), "+v"(G.r0), "+v"(G.hs1), "+v"(G.hs1_pi));
+    asm volatile("" : "+v"(G.th_fac), "+v"(G.d2k), "+v"(G.m2a), "+v"(G.xe2), "+v"(G.xs1));
+#endif
+}
+
 /* The geometry wave of a pair (see above): runs photon after photon -- each begins as a restart
  * request from the interaction wave -- until LONE_STOP. */
-__device__ void lone_geometry(const Params &P, const Ctl &C, int lane, LonePair &pr) {
+__device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair &pr) {
+    Params P = P_;
+    push_params_vgpr(P);
     unsigned gen = 0;
     unsigned long long p = 0, cur = 0, cons = 0; /* cons: the last value read of pr.ctl.cons */
     bool spec = false; /* speculate the halving depths on this step's push (the last one halved) */
@@ -1029,7 +1045,11 @@ __device__ void lone_geometry(const Params &P, const Ctl &C, int lane, LonePair 
                     double e_1;
                     Trig T;
                     Gcov G;
+#ifdef GRM_X_GEO_QUAD
+                    fail = push_attempt_quad<1>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3);
+#else
                     fail = push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
+#endif
                     if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
