@@ -746,6 +746,9 @@ __device__ __forceinline__ double bcast(double v, int src) {
 /* The halving walk proper, on a push state every lane of the wave holds identically (x, k, dk/dlambda,
  * e_0_s; the node `depth` of the halving tree being pushed, the pending second halves `pend`); lane
  * rank r (0 for the state's owner) attempts depth + r.  Leaves the completed push in every lane. */
+/* QUAD: the lone geometry wave's form -- quad r of lanes attempts depth + r with the quad-parallel
+ * push (push_attempt_quad), rank = lane / 4 (16 ranks still cover every depth to MAX_SUBDIV) */
+template <bool QUAD = false>
 __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
                                          double hlen, int depth, uint32_t pend, int rank, int owner) {
     int rounds = 0; /* attempt rounds (diagnostics) */
@@ -759,7 +762,9 @@ __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[
             if (d <= MAX_SUBDIV) {
                 Trig T;
                 Gcov G;
-                const bool fail = push_attempt(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G);
+                const bool fail = QUAD ? push_attempt_quad<1>(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G,
+                                                              (int)(threadIdx.x & 3))
+                                       : push_attempt(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G);
                 ok = !fail || d == MAX_SUBDIV;
             }
             /* the owner's attempt if it passed, else the shallowest passing helper (helper depth grows
@@ -976,6 +981,12 @@ __device__ __forceinline__ void push_params_vgpr(Params &G) {
 #endif
 }
 
+#ifndef GRM_X_NO_GEO_QUAD
+constexpr bool GEO_QUAD = true; /* the geometry wave pushes with quad-parallel corrector rows */
+#else
+constexpr bool GEO_QUAD = false;
+#endif
+
 /* The geometry wave of a pair (see above): runs photon after photon -- each begins as a restart
  * request from the interaction wave -- until LONE_STOP. */
 __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair &pr) {
@@ -1045,11 +1056,9 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
                     double e_1;
                     Trig T;
                     Gcov G;
-#ifdef GRM_X_GEO_QUAD
-                    fail = push_attempt_quad<1>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3);
-#else
-                    fail = push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
-#endif
+                    /* every quad of lanes makes the attempt, lane q contracting connection row q */
+                    fail = GEO_QUAD ? push_attempt_quad<1>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
+                                    : push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
                     if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
@@ -1057,14 +1066,14 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
                             k[i] = kb[i];
                             dk[i] = dkb[i];
                         }
-                        rounds += walk_push(P, x, k, dk, e_0_s, dl, 1, 2u, lane, 0);
+                        rounds += walk_push<GEO_QUAD>(P, x, k, dk, e_0_s, dl, 1, 2u, GEO_QUAD ? lane >> 2 : lane, 0);
                     } else {
                         e_0_s = e_1;
                     }
                 }
                 spec = fail;
             } else {
-                rounds = walk_push(P, x, k, dk, e_0_s, dl, 0, 0u, lane, 0);
+                rounds = walk_push<GEO_QUAD>(P, x, k, dk, e_0_s, dl, 0, 0u, GEO_QUAD ? lane >> 2 : lane, 0);
                 spec = rounds > 1;
             }
         }

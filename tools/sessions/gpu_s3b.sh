@@ -6,8 +6,8 @@
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R" && mkdir -p gpurun_out
 M="$R/tools/microbench"; FL="--offload-arch=gfx950 -O3 -std=c++17 -mllvm -disable-machine-licm -Wno-unused-value -Wno-unused-result -I$R/cuda-grmonty_amd/csrc"
 LK="-L/opt/rocm/lib -lrccl -L$R/cuda-grmonty_amd -lgrmonty_amd -Wl,-rpath,$R/cuda-grmonty_amd"
-/opt/rocm/bin/hipcc $FL $M/geom_only.hip -o /tmp/geo_vg $LK && /opt/rocm/bin/hipcc $FL -DGRM_X_NO_GEO_VGPR $M/geom_only.hip -o /tmp/geo_base $LK || exit 1
-/opt/rocm/bin/hipcc $FL -DGRM_X_GEO_QUAD $M/geom_only.hip -o /tmp/geo_vgq $LK || exit 1
+/opt/rocm/bin/hipcc $FL $M/geom_only.hip -DGRM_X_NO_GEO_QUAD -o /tmp/geo_vg $LK && /opt/rocm/bin/hipcc $FL -DGRM_X_NO_GEO_VGPR -DGRM_X_NO_GEO_QUAD $M/geom_only.hip -o /tmp/geo_base $LK || exit 1
+/opt/rocm/bin/hipcc $FL $M/geom_only.hip -o /tmp/geo_vgq $LK || exit 1
 for v in base vg vgq; do echo "== geom_only $v"; timeout -k 10 60 /tmp/geo_$v || exit 1; done
 for round in 1 2; do for v in base vg vgq; do
   echo "== long photon $v ($round)"
