@@ -69,6 +69,9 @@ __device__ __forceinline__ double fratio_tol(double a, double b) {
  * v_fma_f64 the copy is two s_mov_b32 on the scalar unit: one VALU instruction.  Same operation,
  * same rounding. */
 __device__ __forceinline__ double fma_k(double a, double b, double c) {
+#ifdef GRM_FMA_K_PLAIN
+    return fma(a, b, c);
+#endif
     double d;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
     return d;

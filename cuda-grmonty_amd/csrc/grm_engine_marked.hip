@@ -1031,6 +1031,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
          * restart was pending is dropped (and one published just before a restart carries the
          * old generation's tag, which the interaction wave skips) */
         const unsigned long long req = __hip_atomic_load(&pr.ctl.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile(";;GEO_A");
 #ifdef GRM_TIMING
         const unsigned long long g0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1077,6 +1078,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
                 spec = rounds > 1;
             }
         }
+        asm volatile(";;GEO_B");
         if (req != cur) {
             if (req == LONE_STOP) {
 #ifdef GRM_TIMING
@@ -1563,7 +1565,6 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
     }
 }
 
-#ifdef GRM_LONE_TU
 /* launched on lone_cap workgroups; the launch before handed over *C.lone_count photons */
 __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
     const unsigned long long n_handed = __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1649,9 +1650,6 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-#endif /* GRM_LONE_TU */
-
-#ifndef GRM_LONE_TU
 /* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
  * completed a step, the rest of the while-loop body of track_super_photon
  * (harm_model.cpp:919-1063).  A lane that has to halve its step (push_photon's recursion,
@@ -2344,15 +2342,8 @@ __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
         __threadfence_system();
     }
 }
-#endif /* !GRM_LONE_TU */
 
 } /* namespace */
-
-#ifndef GRM_LONE_TU
-/* lone_kernel / early_kernel live in grm_lone.hip (the same source, compiled without
- * -disable-machine-licm, see there); Params and Ctl cross as bytes */
-extern "C" hipError_t grm_lone_launch(int which, unsigned grid, hipStream_t s, const void *P, size_t p_size,
-                                      const void *C, size_t c_size);
 
 /* ========================================================================= */
 /* engine object + C ABI                                                      */
@@ -2707,12 +2698,14 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.lone_all = e->lone == 2 || (e->lone == 1 && n_pool <= e->lone_cap / 2);
         }
         if (early && e->early_serial) { /* test: serialised ahead of the main launch */
-            HIPCHK(e, grm_lone_launch(1, 1, e->stream, &e->P, sizeof(Params), &C, sizeof(Ctl)));
+            hipLaunchKernelGGL(early_kernel, dim3(1), dim3(64 * 2 * LONE_PAIRS), 0, e->stream, e->P, C);
+            HIPCHK(e, hipGetLastError());
             HIPCHK(e, hipEventRecord(e->ev_w, e->stream));
         } else if (early) { /* after the control words are set; one workgroup, all of its pairs */
             HIPCHK(e, hipEventRecord(e->ev_pre, e->stream));
             HIPCHK(e, hipStreamWaitEvent(e->stream2, e->ev_pre, 0));
-            HIPCHK(e, grm_lone_launch(1, 1, e->stream2, &e->P, sizeof(Params), &C, sizeof(Ctl)));
+            hipLaunchKernelGGL(early_kernel, dim3(1), dim3(64 * 2 * LONE_PAIRS), 0, e->stream2, e->P, C);
+            HIPCHK(e, hipGetLastError());
             HIPCHK(e, hipEventRecord(e->ev_w, e->stream2));
         }
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
@@ -2727,7 +2720,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
          * children join this launch's overflow pool */
         if (C.lone) {
             HIPCHK(e, hipEventRecord(e->ev2, e->stream));
-            HIPCHK(e, grm_lone_launch(0, (unsigned)e->lone_cap, e->stream, &e->P, sizeof(Params), &C, sizeof(Ctl)));
+            hipLaunchKernelGGL(lone_kernel, dim3((unsigned)e->lone_cap), dim3(128), 0, e->stream, e->P, C);
+            HIPCHK(e, hipGetLastError());
             HIPCHK(e, hipEventRecord(e->ev3, e->stream));
         }
         if (early) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_w, 0)); /* its photons' counters too */
@@ -3610,4 +3604,3 @@ size_t grm_sizeof(int which) {
 const char *grm_version(void) { return "grmonty_amd 0.1.0 (gfx950)"; }
 
 } /* extern "C" */
-#endif /* !GRM_LONE_TU */

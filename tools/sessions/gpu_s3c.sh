@@ -5,7 +5,7 @@
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R" && mkdir -p gpurun_out
 T=s3c
 : timeout -k 10 600 python -u -m pytest tests/test_gpu_transport.py tests/test_gpu_probes.py -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1
-: pytest ran in the first s3c call (18 passed)
+# pytest ran in the first s3c call: 18 passed
 M="$R/tools/microbench"; FL="--offload-arch=gfx950 -O3 -std=c++17 -mllvm -disable-machine-licm -Wno-unused-value -Wno-unused-result -I$R/cuda-grmonty_amd/csrc"
 LK="-L/opt/rocm/lib -lrccl -L$R/cuda-grmonty_amd -lgrmonty_amd -Wl,-rpath,$R/cuda-grmonty_amd"
 /opt/rocm/bin/hipcc $FL $M/geom_only.hip -o /tmp/geo_q $LK && /opt/rocm/bin/hipcc $FL -DGRM_X_NO_GEO_QUAD $M/geom_only.hip -o /tmp/geo_vg $LK || exit 1
