@@ -169,8 +169,8 @@ constexpr int LANE_XFIELDS = 10;
     X(n_scatt, 0)                                                                                    \
     X(flight, 1) /* warm-up: photons started (+) / ended (-) since the last flush */                \
     /* the lane's launch counters (widened and wave-reduced at exit) */                              \
-    X(c_steps, 2) X(c_tracked, 3) X(c_primaries, 4) X(c_children, 5) X(c_nstep_max, 6) X(c_long, 7)
-constexpr int LANE_IFIELDS = 8;
+    X(c_tracked, 2) X(c_primaries, 3) X(c_children, 4) X(c_nstep_max, 5) X(c_long, 6)
+constexpr int LANE_IFIELDS = 7;
 /* [field][lane], indexed with threadIdx.x so that every access is one ds_read/ds_write_b64 with an
  * immediate offset (a generic pointer here would turn them into FLAT accesses, which also count in
  * vmcnt and cost a 64-bit address register each) */
@@ -748,6 +748,9 @@ __device__ __forceinline__ double bcast(double v, int src) {
  * rank r (0 for the state's owner) attempts depth + r.  Leaves the completed push in every lane. */
 /* QUAD: the lone geometry wave's form -- quad r of lanes attempts depth + r with the quad-parallel
  * push (push_attempt_quad), rank = lane / 4 (16 ranks still cover every depth to MAX_SUBDIV) */
+#ifndef GRM_X_GEO_ROWS
+#define GRM_X_GEO_ROWS 1 /* connection rows to the quad lanes: 1 selected from all four, 0 divergent blocks */
+#endif
 template <bool QUAD = false>
 __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
                                          double hlen, int depth, uint32_t pend, int rank, int owner) {
@@ -762,7 +765,7 @@ __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[
             if (d <= MAX_SUBDIV) {
                 Trig T;
                 Gcov G;
-                const bool fail = QUAD ? push_attempt_quad<1>(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G,
+                const bool fail = QUAD ? push_attempt_quad<GRM_X_GEO_ROWS>(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G,
                                                               (int)(threadIdx.x & 3))
                                        : push_attempt(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G);
                 ok = !fail || d == MAX_SUBDIV;
@@ -1057,7 +1060,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
                     Trig T;
                     Gcov G;
                     /* every quad of lanes makes the attempt, lane q contracting connection row q */
-                    fail = GEO_QUAD ? push_attempt_quad<1>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
+                    fail = GEO_QUAD ? push_attempt_quad<GRM_X_GEO_ROWS>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
                                     : push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
                     if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
 #pragma unroll
@@ -1659,7 +1662,7 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
  * whole wave waiting for the deepest halving tree.  `walked`: halving_walk has just completed this
  * lane's push (its phase-0 block ran before it).  Returns false when the photon's life ended. */
 __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *cold, SReq *wstack, int *wtop,
-                               const Slot &ph2, const Slot &bk, double bias_d, bool walked) {
+                               const Slot &ph2, const Slot &bk, double bias_d, bool walked, bool &stepped) {
     if (L.phase == 0 && !trip_begin(P, C, L, cold, ph2)) return false;
     TSTAMP(8);
     /* one attempt of push_photon at the current node of the halving tree (:1217-1289).  A lane in
@@ -1709,7 +1712,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
      * ONE evaluation here so a wave with lanes in both phases runs that code once. */
     const bool at_scatter = L.phase == 2;
     if (!at_scatter && !setup) {
-        ++L.c_steps();
+        stepped = true; /* counted per wave by the caller (a ballot), not per lane in LDS */
         if (stop_criterion(P, L)) {
             end_of_life(P, C, cold, L);
             return false;
@@ -1909,7 +1912,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     unsigned trip = 1;
     /* per-lane launch counters, 32-bit in the loop (a lane makes < 2^32 steps per launch), widened
      * for the wave reduction at exit */
-    L.c_steps() = L.c_tracked() = L.c_primaries() = L.c_children() = 0;
+    L.c_tracked() = L.c_primaries() = L.c_children() = 0;
+    unsigned long long wave_steps = 0; /* wave-uniform: transport steps the wave's lanes completed */
     L.c_nstep_max() = L.c_long() = 0; /* longest photon life; lives > 100k steps */
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
 
@@ -2180,14 +2184,16 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 }
             }
         }
+        bool stepped = false;
         if (active) {
-            active = !ended && transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked);
+            active = !ended && transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked, stepped);
             if (!active) {
                 L.c_nstep_max() = max((int)L.c_nstep_max(), L.n_step);
                 L.c_long() += L.n_step > 100000 ? 1 : 0;
                 --L.flight();
             }
         }
+        wave_steps += (unsigned long long)__popcll(__ballot(stepped)); /* scalar: no LDS round trip per step */
         if (warm) {
             int d = L.flight();
 #pragma unroll
@@ -2219,12 +2225,11 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         if (v != 0.0) unsafeAtomicAdd(reinterpret_cast<double *>(C.spec + i / SPEC_CELL) + (i & (SPEC_CELL - 1)), v);
     }
     /* wave-reduce the lane counters, one atomic per wave */
-    unsigned long long w_steps = (unsigned)L.c_steps(), w_tracked = (unsigned)L.c_tracked();
+    unsigned long long w_tracked = (unsigned)L.c_tracked();
     unsigned long long w_primaries = (unsigned)L.c_primaries(), w_children = (unsigned)L.c_children();
     unsigned long long w_long = (unsigned)L.c_long(), w_nstep_max = (unsigned)L.c_nstep_max();
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        w_steps += __shfl_xor(w_steps, off);
         w_tracked += __shfl_xor(w_tracked, off);
         w_primaries += __shfl_xor(w_primaries, off);
         w_children += __shfl_xor(w_children, off);
@@ -2232,7 +2237,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         w_nstep_max = max(w_nstep_max, (unsigned long long)__shfl_xor(w_nstep_max, off));
     }
     if (lane_id == 0) {
-        atomicAdd(&C.ctr->n_steps, w_steps);
+        atomicAdd(&C.ctr->n_steps, wave_steps);
         atomicAdd(&C.ctr->n_tracked, w_tracked);
         atomicAdd(&C.ctr->n_primaries, w_primaries);
         atomicAdd(&C.ctr->n_children, w_children);
