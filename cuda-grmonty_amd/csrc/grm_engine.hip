@@ -119,6 +119,8 @@ struct Ctl {
     int admit_slack;
     unsigned long long admit_b0; /* first batch */
     unsigned long long admit_spread; /* photons one wave claims at most per warm-up claim (0: no cap) */
+    unsigned warm_blocks, warm_waves; /* the waves that take the warm-up's batches: blockIdx < warm_blocks,
+                                       * wave-in-workgroup < warm_waves (the rest park) */
     unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     unsigned long long *phases; /* s_memrealtime when the warm-up admission ended ([0]) and the pool's
@@ -1923,7 +1925,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         const Ctl &C = karg_ctl(kt);
         ++wave_trips;
         TCOUNT(4);
-        if (warm && blockIdx.x >= WARM_BLOCKS) {
+        if (warm && (blockIdx.x >= C.warm_blocks || (unsigned)wave >= C.warm_waves)) {
             /* the warm-up's admission batches are small: the waves of the first WARM_BLOCKS
              * workgroups take them, the rest wait here without touching the counters (their polling
              * would contend with the warm-up's own counter traffic) until the admission is over */
@@ -2440,6 +2442,7 @@ struct grm_engine {
      * WARMUP_PHOTONS warm-up; none for the ramp to a grid of lanes (its batches outnumber the
      * warm-up's lanes) */
     int64_t warmup_spread = -1;
+    int64_t warmup_blocks = 0, warmup_waves = 0; /* GRM_OPT_WARMUP_BLOCKS / _WAVES (0 = default) */
     /* host-mapped control block: ctl_kernel mirrors the counters and the small words here (ctr,
      * small) and the emission scan writes its total (word[4]); the host reads them after a stream
      * synchronisation, so a pass runs without copy or fill kernels (see ctl_kernel) */
@@ -2632,6 +2635,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.admit_b0 = e->warmup_b0;
         C.admit_spread = e->warmup_spread >= 0 ? (unsigned long long)e->warmup_spread
                                                : (e->warmup == -2 && small ? 0ull : WARMUP_SPREAD);
+        C.warm_blocks = e->warmup_blocks > 0 ? (unsigned)e->warmup_blocks : WARM_BLOCKS;
+        C.warm_waves = e->warmup_waves > 0 ? (unsigned)e->warmup_waves : (unsigned)(BLOCK / 64);
     }
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
@@ -3023,6 +3028,8 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
     case GRM_OPT_WARMUP_SPREAD: e->warmup_spread = v < 0 ? -1 : v; return 0;
+    case GRM_OPT_WARMUP_BLOCKS: e->warmup_blocks = v < 0 ? 0 : v; return 0;
+    case GRM_OPT_WARMUP_WAVES: e->warmup_waves = v < 0 ? 0 : (v > BLOCK / 64 ? BLOCK / 64 : v); return 0;
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;

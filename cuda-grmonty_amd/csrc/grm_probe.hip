@@ -27,6 +27,9 @@
  * 20     x                                          fsincospi(x) s c, ocml sincospi(x) s c
  * 21     x                                          fexp(x), ocml exp(x)
  * 22     x                                          fexp10(x), ocml exp10(x)
+ * 23     x[4] k[4] dk[4] e_0_s dl                   one push attempt: push_attempt x k dk e_1 fail (14), then
+ *                                                   push_attempt_quad's (14; four lanes per item, lane q
+ *                                                   contracting connection row q -- the lone geometry wave's push)
  */
 #include <hip/hip_runtime.h>
 
@@ -42,6 +45,39 @@ namespace {
 __device__ void store(double *o, int k, double v) { o[k] = v; }
 
 __global__ void probe_kernel(Params P, int which, const double *in, int is, double *out, int os, size_t n) {
+    if (which == 23) { /* four lanes per item (the launch has 4 n lanes, quads never straddle an item) */
+        const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+        const int q = (int)(threadIdx.x & 3);
+        if (t >= n) return;
+        const double *a = in + t * is;
+        double *o = out + t * os;
+        double x[4], k[4], dk[4], xq[4], kq[4], dkq[4];
+        for (int i = 0; i < 4; ++i) {
+            x[i] = xq[i] = a[i];
+            k[i] = kq[i] = a[4 + i];
+            dk[i] = dkq[i] = a[8 + i];
+        }
+        double e1, e1q;
+        Trig T;
+        Gcov G;
+        const bool f = push_attempt(P, x, k, dk, a[12], a[13], e1, T, G);
+        const bool fq = push_attempt_quad<1>(P, xq, kq, dkq, a[12], a[13], e1q, T, G, q);
+        if (q == 0) {
+            for (int i = 0; i < 4; ++i) {
+                store(o, i, x[i]);
+                store(o, 4 + i, k[i]);
+                store(o, 8 + i, dk[i]);
+                store(o, 14 + i, xq[i]);
+                store(o, 18 + i, kq[i]);
+                store(o, 22 + i, dkq[i]);
+            }
+            store(o, 12, e1);
+            store(o, 13, f ? 1.0 : 0.0);
+            store(o, 26, e1q);
+            store(o, 27, fq ? 1.0 : 0.0);
+        }
+        return;
+    }
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const double *a = in + t * is;
@@ -239,7 +275,7 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
 extern "C" int grm_probe_impl(const Params &P, hipStream_t s, int which, const double *in, int in_stride, double *out,
                               int out_stride, size_t n, std::string &err) {
     if (n == 0) return 0;
-    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 22) {
+    if (!in || !out || in_stride < 1 || out_stride < 1 || which < 0 || which > 23 || (which == 23 && out_stride < 28)) {
         err = "grm_probe: bad arguments";
         return -1;
     }
@@ -250,7 +286,8 @@ extern "C" int grm_probe_impl(const Params &P, hipStream_t s, int which, const d
     if (st == hipSuccess) st = hipMemsetAsync(d_out, 0, n * out_stride * sizeof(double), s);
     if (st == hipSuccess) {
         const int B = 64;
-        hipLaunchKernelGGL(probe_kernel, dim3((unsigned)((n + B - 1) / B)), dim3(B), 0, s, P, which, d_in, in_stride,
+        const size_t lanes = which == 23 ? 4 * n : n;
+        hipLaunchKernelGGL(probe_kernel, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), 0, s, P, which, d_in, in_stride,
                            d_out, out_stride, n);
         st = hipGetLastError();
     }

@@ -55,6 +55,8 @@ OPT_EARLY_SERIAL = 16
 OPT_KARG_TEST = 17
 OPT_LONE_K = 18
 OPT_WARMUP_SPREAD = 19
+OPT_WARMUP_BLOCKS = 20
+OPT_WARMUP_WAVES = 21
 N_TH_BINS, N_E_BINS = 6, 200
 
 

@@ -181,7 +181,12 @@ enum {
     /* a wave claims at most this many photons of a warm-up admission batch at a time, spreading the
      * batch, and its photons' scattering families, over more waves (0: as many lanes as it has idle;
      * -1, the default: 4 in the 4,096-photon warm-up, 0 in the ramp of a small pass) */
-    GRM_OPT_WARMUP_SPREAD = 19
+    GRM_OPT_WARMUP_SPREAD = 19,
+    /* the waves that take the warm-up's admission batches (the others park until it is over):
+     * the first this-many workgroups (0 or default: 64; larger values are capped at the grid) ... */
+    GRM_OPT_WARMUP_BLOCKS = 20,
+    /* ... and of each, its first this-many waves (1..8; 0 or default: all 8) */
+    GRM_OPT_WARMUP_WAVES = 21
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

@@ -122,6 +122,42 @@ def test_push_photon(engine, oracle64, samples):
     assert bad <= max(2, len(allst) // 200), f"{bad}/{len(allst)} pushes differ"
 
 
+def test_quad_push_attempt(engine, oracle64, samples):
+    """push_attempt_quad (grm_device.h: the lone geometry wave's push, four lanes per attempt, lane q
+    contracting connection row q, k and the tolerance ratios exchanged by DPP) against push_attempt
+    on the same inputs: the same fail decisions and the same state to ~1 ulp (each row is contracted
+    with the reference's expression, harm_model.cpp:1255-1266, and the ratios summed in its order; only
+    the compiler's FMA contraction of a row may differ), at the transport's step lengths and 8x them."""
+    O, L = _o()
+    sel, _, _ = samples
+    n = len(sel)
+    st = np.zeros((n, 14))
+    st[:, 0:4] = sel["x"]
+    st[:, 4:8] = sel["k"]
+    for i in range(n):
+        dk = np.zeros(4)
+        L.grmo_init_dkdlam(oracle64.h, np.ascontiguousarray(st[i, :4]).ctypes.data_as(DP),
+                           np.ascontiguousarray(st[i, 4:8]).ctypes.data_as(DP), dk.ctypes.data_as(DP))
+        st[i, 8:12] = dk
+        st[i, 12] = sel["e"][i]
+        st[i, 13] = L.grmo_step_size(oracle64.h, np.ascontiguousarray(st[i, :4]).ctypes.data_as(DP),
+                                     np.ascontiguousarray(st[i, 4:8]).ctypes.data_as(DP))
+    st2 = st.copy()
+    st2[:, 13] *= 8.0
+    allst = np.concatenate([st, st2])
+    dev = engine.probe(23, allst, 28)
+    plain, quad = dev[:, :14], dev[:, 14:28]
+    assert np.all(np.isfinite(plain[:, :13]))
+    assert (plain[:, 13] != quad[:, 13]).sum() <= max(1, len(allst) // 500)
+    scale = np.maximum(np.abs(plain[:, :13]), 1e-300)
+    rel = np.abs(quad[:, :13] - plain[:, :13]) / scale
+    same = plain[:, 13] == quad[:, 13]
+    print(f"quad push: {same.mean():.4f} same decisions, max rel diff {rel[same].max():.2e}, "
+          f"bit-identical states {np.all(quad[:, :13] == plain[:, :13], axis=1).mean():.3f}, "
+          f"{int(plain[:, 13].sum())} failing attempts of {len(allst)}")
+    assert rel[same].max() < 1e-12
+
+
 def test_fluid_and_radiation(engine, oracle64, samples):
     O, L = _o()
     _, x, k = samples
