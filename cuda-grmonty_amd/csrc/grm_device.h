@@ -610,7 +610,25 @@ __device__ __forceinline__ void connection_quad_sel(const Params &P, const Trig 
     }
 }
 
-/* push_attempt on a quad (q = lane & 3; x, k, dk, e_0_s identical over the quad on entry and exit) */
+/* row q from two exec-masked blocks of two rows each (lanes 0-1 form rows 0, 1; lanes 2-3 rows 2, 3):
+ * the rows of a block interleave, and one select per 32-bit half picks the lane's row (20 selects) */
+__device__ __forceinline__ void connection_quad_half(const Params &P, const Trig &T, int q, double L[10]) {
+    ConnPre Q;
+    connection_pre(P, T, Q);
+    double A[10], B[10];
+    if (q < 2) {
+        connection_row(Q, 0, A);
+        connection_row(Q, 1, B);
+    } else {
+        connection_row(Q, 2, A);
+        connection_row(Q, 3, B);
+    }
+#pragma unroll
+    for (int j = 0; j < 10; ++j) L[j] = (q & 1) ? B[j] : A[j];
+}
+
+/* push_attempt on a quad (q = lane & 3; x, k, dk, e_0_s identical over the quad on entry and exit);
+ * ROWS: how row q reaches lane q (0 divergent blocks, 1 selected from all four rows, 2 two blocks of two) */
 template <int ROWS = 0>
 __device__ __forceinline__ bool push_attempt_quad(const Params &P, double x[4], double k[4], double dk[4],
                                                   double e_0_s, double dl, double &e_1, Trig &T, Gcov &G, int q) {
@@ -620,8 +638,10 @@ __device__ __forceinline__ bool push_attempt_quad(const Params &P, double x[4], 
     double L[10];
     if (ROWS == 0)
         connection_quad_row(P, T, q, L);
-    else
+    else if (ROWS == 1)
         connection_quad_sel(P, T, q, L);
+    else
+        connection_quad_half(P, T, q, L);
     gcov_from_trig(P, T, G);
     const double dl_2 = 0.5 * dl;
     const double kq = quad_pick(k, q); /* the half-kicked k^q */

@@ -751,7 +751,7 @@ __device__ __forceinline__ double bcast(double v, int src) {
 /* QUAD: the lone geometry wave's form -- quad r of lanes attempts depth + r with the quad-parallel
  * push (push_attempt_quad), rank = lane / 4 (16 ranks still cover every depth to MAX_SUBDIV) */
 #ifndef GRM_X_GEO_ROWS
-#define GRM_X_GEO_ROWS 1 /* connection rows to the quad lanes: 1 selected from all four, 0 divergent blocks */
+#define GRM_X_GEO_ROWS 2 /* connection rows to the quad lanes: 2 two blocks of two rows (1.34-1.35 us/step on the long photon), 1 selected from all four (1.37-1.38), 0 four divergent blocks (1.38-1.41) */
 #endif
 template <bool QUAD = false>
 __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
