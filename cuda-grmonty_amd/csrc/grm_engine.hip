@@ -2748,6 +2748,11 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         ms_total += ms;
         const unsigned long long n_lone = std::min<unsigned long long>(e->pin->small[7], e->lone_cap);
         if (early) e->stats.n_early += std::min<unsigned long long>(e->pin->small[8], grm_engine::EARLY_CAP);
+        if (early && !e->early_serial) { /* ev_pre (engine stream, before the bulk) .. ev_w (after the worker) */
+            float ms_e = 0.f;
+            HIPCHK(e, hipEventElapsedTime(&ms_e, e->ev_pre, e->ev_w));
+            if (ms_e > e->stats.early_ms) e->stats.early_ms = ms_e;
+        }
         if (C.lone) {
             float ms_l = 0.f;
             HIPCHK(e, hipEventElapsedTime(&ms_l, e->ev2, e->ev3));
@@ -2864,8 +2869,8 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
     if (!hip_ok(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking), "stream")) return fail();
     if (!hip_ok(e, hipEventCreate(&e->ev0), "event") || !hip_ok(e, hipEventCreate(&e->ev1), "event") ||
         !hip_ok(e, hipEventCreate(&e->ev2), "event") || !hip_ok(e, hipEventCreate(&e->ev3), "event") ||
-        !hip_ok(e, hipEventCreateWithFlags(&e->ev_pre, hipEventDisableTiming), "event") ||
-        !hip_ok(e, hipEventCreateWithFlags(&e->ev_w, hipEventDisableTiming), "event") ||
+        !hip_ok(e, hipEventCreate(&e->ev_pre), "event") || /* timed: stats.early_ms */
+        !hip_ok(e, hipEventCreate(&e->ev_w), "event") ||
         !hip_ok(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking), "stream") ||
         !hip_ok(e, hipMalloc(&e->d_early, grm_engine::EARLY_CAP * sizeof(LoneRec)), "early queue") ||
         !hip_ok(e, hipMalloc(&e->d_early_ready, grm_engine::EARLY_CAP * sizeof(unsigned long long)), "early queue") ||

@@ -82,7 +82,7 @@ class Stats(C.Structure):
                 ("max_launch_ms", C.c_double), ("max_launch_steps", C.c_uint64),
                 ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64), ("n_abandoned", C.c_uint64),
                 ("n_nan_photons", C.c_uint64), ("n_lone", C.c_uint64), ("lone_ms", C.c_double),
-                ("n_early", C.c_uint64)]
+                ("n_early", C.c_uint64), ("early_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

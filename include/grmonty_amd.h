@@ -120,6 +120,7 @@ typedef struct grm_stats {
     uint64_t n_lone;           /* photons handed over to the lone-photon kernel since the last reset */
     double lone_ms;            /* time in lone-photon kernel launches since the last reset */
     uint64_t n_early;          /* long photons handed to the concurrent early worker since the last reset */
+    double early_ms;           /* the early worker's longest launch (its stream's events) since the last reset */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
