@@ -750,9 +750,10 @@ __device__ __forceinline__ double bcast(double v, int src) {
  * rank r (0 for the state's owner) attempts depth + r.  Leaves the completed push in every lane. */
 /* QUAD: the lone geometry wave's form -- quad r of lanes attempts depth + r with the quad-parallel
  * push (push_attempt_quad), rank = lane / 4 (16 ranks still cover every depth to MAX_SUBDIV) */
-#ifndef GRM_X_GEO_ROWS
-#define GRM_X_GEO_ROWS 2 /* connection rows to the quad lanes: 2 two blocks of two rows (1.34-1.35 us/step on the long photon), 1 selected from all four (1.37-1.38), 0 four divergent blocks (1.38-1.41) */
-#endif
+/* how connection row q reaches lane q of the lone geometry wave's quads (push_attempt_quad): two
+ * blocks of two rows (1.34-1.35 us/step on the long photon; selected from all four rows 1.37-1.38,
+ * four divergent blocks 1.38-1.41, profiles/r03_ab/s3e_*, s3h_*) */
+constexpr int GEO_ROWS = 2;
 template <bool QUAD = false>
 __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
                                          double hlen, int depth, uint32_t pend, int rank, int owner) {
@@ -767,7 +768,7 @@ __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[
             if (d <= MAX_SUBDIV) {
                 Trig T;
                 Gcov G;
-                const bool fail = QUAD ? push_attempt_quad<GRM_X_GEO_ROWS>(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G,
+                const bool fail = QUAD ? push_attempt_quad<GEO_ROWS>(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G,
                                                               (int)(threadIdx.x & 3))
                                        : push_attempt(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G);
                 ok = !fail || d == MAX_SUBDIV;
@@ -980,17 +981,12 @@ __device__ __forceinline__ bool kargs_check(KArgsK *ka, const Params &P, const C
  * VGPR pairs instead (26 VGPRs of the 512 a single wave per SIMD has) and feed the fp64 VALU
  * directly.  Same values, same operations. */
 __device__ __forceinline__ void push_params_vgpr(Params &G) {
-#ifndef GRM_X_NO_GEO_VGPR
     asm volatile("" : "+v"(G.a), "+v"(G.a2), "+v"(G.a3), "+v"(G.a4), "+v"(G.r0), "+v"(G.hs1), "+v"(G.hs1_pi));
     asm volatile("" : "+v"(G.th_fac), "+v"(G.d2k), "+v"(G.m2a), "+v"(G.xe2), "+v"(G.xs1));
-#endif
 }
 
-#ifndef GRM_X_NO_GEO_QUAD
-constexpr bool GEO_QUAD = true; /* the geometry wave pushes with quad-parallel corrector rows */
-#else
-constexpr bool GEO_QUAD = false;
-#endif
+constexpr bool GEO_QUAD = true; /* the geometry wave pushes with quad-parallel corrector rows (§4.2:
+                                   * the plain push 1.41-1.42 us/step against 1.36-1.37, s3e) */
 
 /* The geometry wave of a pair (see above): runs photon after photon -- each begins as a restart
  * request from the interaction wave -- until LONE_STOP. */
@@ -1062,7 +1058,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
                     Trig T;
                     Gcov G;
                     /* every quad of lanes makes the attempt, lane q contracting connection row q */
-                    fail = GEO_QUAD ? push_attempt_quad<GRM_X_GEO_ROWS>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
+                    fail = GEO_QUAD ? push_attempt_quad<GEO_ROWS>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
                                     : push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
                     if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
 #pragma unroll

@@ -12,9 +12,7 @@
  * ~100 fewer instructions.  Same operations, same results.
  */
 #define GRM_LONE_TU 1
-#ifndef GRM_X_LONE_ASM_K
 #define GRM_FMA_K_PLAIN 1
-#endif
 #include "grm_engine.hip"
 
 extern "C" hipError_t grm_lone_launch(int which, unsigned grid, hipStream_t s, const void *P, size_t p_size,
