@@ -192,6 +192,15 @@ def main():
         import torch
         import torch.distributed as dist
         dist.init_process_group("gloo")
+        # one GPU per rank; with more ranks than GPUs (a rehearsal on a smaller box) ranks share them
+        # round-robin (counting devices does not initialise the GPU on this image)
+        n_dev = torch.cuda.device_count()
+        if n_dev and local >= n_dev:
+            local = local % n_dev
+    # ranks sharing a GPU (a rehearsal with more ranks than GPUs): RCCL refuses two ranks on one
+    # device, so the job's one reduction of the stashed passes goes over gloo instead, with the same
+    # sum / max split of the engine's packing (tests/test_gpu_multirank.py reduces it the same way)
+    shared_gpu = False
     threads = args.threads or host_threads(world)
     photon_n_job = int(args.photon_n) * (world if args.scaling == "weak" else 1)
     path = args.dump or os.path.join(REPO, "gpurun_out" if os.path.isdir(os.path.join(REPO, "gpurun_out")) else ".",
@@ -217,9 +226,13 @@ def main():
         k, v = kv.split("=")
         engine.set_option(int(k), int(v))
     if world > 1:  # one RCCL communicator per rank
-        uid = [G.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        engine.comm_init(uid[0], world, rank)
+        devs = [None] * world
+        dist.all_gather_object(devs, local)
+        shared_gpu = len(set(devs)) < world
+        if not shared_gpu:
+            uid = [G.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            engine.comm_init(uid[0], world, rank)
     engine.emit_setup(model)  # the zone table is resident in HBM before the timed region
     bias_counters = "single GPU"
     if world > 1:
@@ -271,7 +284,16 @@ def main():
         """the job's one exchange: a grouped RCCL all-reduce of every pass's stashed results, then
         each pass's reduced spectrum and counters read back (the ranks' pass timelines stay
         uncoupled: a rank held up by a long-lived photon does not stall the others pass by pass)"""
-        eng.allreduce_stash(first + n)
+        if shared_gpu:
+            spec, sums, maxs = eng.stash_raw(n, first)
+            ts, tu = torch.from_numpy(spec), torch.from_numpy(sums.view(np.int64))
+            tm = torch.from_numpy(maxs.view(np.int64))
+            dist.all_reduce(ts, op=dist.ReduceOp.SUM)
+            dist.all_reduce(tu, op=dist.ReduceOp.SUM)
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)  # every word < 2^63: int64 order = u64 order
+            eng.stash_raw_write(ts.numpy(), tu.numpy().view(np.uint64), tm.numpy().view(np.uint64), first)
+        else:
+            eng.allreduce_stash(first + n)
         return [eng.stash_read(first + s) for s in range(n)]
 
     for i, sd in enumerate(warm_seeds):
@@ -367,8 +389,10 @@ def main():
                        "photon_n_job": photon_n_job, "grid": f"{args.grid}x{args.grid}",
                        "superphotons_per_pass_rank0": n_rank // max(1, args.steps),
                        "bias_counters": bias_counters,
-                       "parallelism": f"strided zone shards x{world}" + (", passes stashed on the device, one RCCL all-reduce per job"
-                                                                  if world > 1 else "")},
+                       "parallelism": f"strided zone shards x{world}" + (
+                           (", ranks sharing GPUs (rehearsal): passes stashed on the device, one gloo reduction per job"
+                            if shared_gpu else ", passes stashed on the device, one RCCL all-reduce per job")
+                           if world > 1 else "")},
             "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": achieved_tf / FP64_PEAK_TFS if achieved_tf else None,
                          "traffic": traffic,
