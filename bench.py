@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--photon-n", type=float, default=1e6,
                     help="photon_n per GPU (--scaling weak) or of the whole job (--scaling strong)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--shard-of", default="",
+                    help="R/N: run only rank R's zone shard of an N-rank job on this one GPU (a rehearsal of one "
+                         "rank of BASELINE configs[3] -- photon_n 1e8 over 8 GPUs -- without the other ranks)")
     ap.add_argument("--grid", type=int, default=192)
     ap.add_argument("--dump", default="", help="HARM dump to use (default: synthetic dump019-class)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
@@ -201,8 +204,17 @@ def main():
     # device, so the job's one reduction of the stashed passes goes over gloo instead, with the same
     # sum / max split of the engine's packing (tests/test_gpu_multirank.py reduces it the same way)
     shared_gpu = False
+    devs = [local]
     threads = args.threads or host_threads(world)
-    photon_n_job = int(args.photon_n) * (world if args.scaling == "weak" else 1)
+    # the partition: the job's ranks, and this process's place in it (--shard-of R/N: one rank of an
+    # N-rank job alone on this GPU)
+    part_rank, part_world = rank, world
+    if args.shard_of:
+        if world != 1:
+            raise SystemExit("--shard-of runs one rank's shard in a single process")
+        part_rank, part_world = (int(v) for v in args.shard_of.split("/"))
+        assert 0 <= part_rank < part_world
+    photon_n_job = int(args.photon_n) * (part_world if args.scaling == "weak" else 1)
     path = args.dump or os.path.join(REPO, "gpurun_out" if os.path.isdir(os.path.join(REPO, "gpurun_out")) else ".",
                                      f"synth{args.grid}_r{rank}.dump")
     if not args.dump:
@@ -210,15 +222,15 @@ def main():
     t = time.time()
     model = G.Model.load(path, photon_n=photon_n_job).init(threads, device=local)
     t_init = time.time() - t
-    shards = G.zone_shards(model.zone_weights(), world, "strided")
-    z0, z1, zst = shards[rank]
+    shards = G.zone_shards(model.zone_weights(), part_world, "strided")
+    z0, z1, zst = shards[part_rank]
     timed_seeds = [SEED0 + s for s in range(args.steps)]
     warm_seeds = [WARM_SEED0 + s for s in range(args.warmup)]
     # per-seed photon counts of every shard (host, outside the timing): the rank's id base
     t = time.time()
     id_base = {}
     for sd in warm_seeds + timed_seeds:
-        id_base[sd] = sum(model.count(seed=sd, z0=a, z1=b, threads=threads, stride=st) for a, b, st in shards[:rank])
+        id_base[sd] = sum(model.count(seed=sd, z0=a, z1=b, threads=threads, stride=st) for a, b, st in shards[:part_rank])
     t_count = time.time() - t
     engine = G.Engine(model, device=local)
     # A/B hook: GRM_BENCH_OPTS="15=2000,9=2" sets engine options (grmonty_amd.OPT_*) before the passes
@@ -235,6 +247,14 @@ def main():
             engine.comm_init(uid[0], world, rank)
     engine.emit_setup(model)  # the zone table is resident in HBM before the timed region
     bias_counters = "single GPU"
+    valid_for_parity = True
+    # pre-flight: which of the job's GPUs this rank can read over xGMI (hipDeviceCanAccessPeer)
+    peer_row = [int(d == local or G.lib().grm_device_peer_ok(local, d) == 1) for d in sorted(set(devs))]
+    peer_matrix = [peer_row]
+    if world > 1:
+        rows = [None] * world
+        dist.all_gather_object(rows, (local, peer_row))
+        peer_matrix = [r for _, r in sorted(dict(rows).items())]
     if world > 1:
         # pass slots: warm-up passes 0..W-1, timed passes W..W+K-1 (each pass its own counter block)
         engine.stash_reserve(len(warm_seeds) + len(timed_seeds))
@@ -246,7 +266,7 @@ def main():
         devices = [None] * world
         dist.all_gather_object(devices, local)
         # every rank's GPU must be readable from this one (xGMI peer access) before its blocks are mapped
-        ok = all(G.lib().grm_device_peer_ok(local, d) == 1 for d in devices)
+        ok = all(d == local or G.lib().grm_device_peer_ok(local, d) == 1 for d in devices)
         if ok:
             try:
                 engine.set_peers(handles, rank)
@@ -260,6 +280,13 @@ def main():
         if not all(flags):
             engine.set_peers([], rank)
         bias_counters = "job-wide (peer counter blocks over xGMI)" if all(flags) else "per rank (IPC unavailable)"
+        if not all(flags):
+            # not silent: per-rank counters run each rank's adaptive bias on a history N times shorter
+            # (recorded +18/+30/+35 % at 2/4/8 ranks) -- the line says so
+            valid_for_parity = False
+            if rank == 0:
+                print("WARNING: job-wide bias counters unavailable (no peer access / IPC); the counters of this "
+                      "job are NOT the reference's (valid_for_parity=false)", file=sys.stderr, flush=True)
 
     def one_pass(eng, seed, base, slot):
         """one run_simulation pass on this rank's shard: emission + transport + readback; with
@@ -293,7 +320,7 @@ def main():
             dist.all_reduce(tm, op=dist.ReduceOp.MAX)  # every word < 2^63: int64 order = u64 order
             eng.stash_raw_write(ts.numpy(), tu.numpy().view(np.uint64), tm.numpy().view(np.uint64), first)
         else:
-            eng.allreduce_stash(first + n)
+            eng.allreduce_stash(n, first)
         return [eng.stash_read(first + s) for s in range(n)]
 
     for i, sd in enumerate(warm_seeds):
@@ -374,7 +401,8 @@ def main():
             "metric": "superphotons/sec on dump019-class HARM dump (photon_n=1e6 per run_simulation)",
             "value": total / tmax,
             "unit": "superphotons/s",
-            "n_gpus": world,
+            "n_gpus": len(set(devs)),
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": tmax / args.steps * 1e3,
@@ -385,10 +413,14 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"synthetic dump019-class {args.grid}x{args.grid} MKS HARM dump, photon_n="
                                    f"{photon_n_job:g} run_simulation passes (seeds {SEED0}..{SEED0 + args.steps - 1}), "
-                                   f"mass_unit=4e19, zone-sharded over {world} GPU(s)",
+                                   f"mass_unit=4e19, zone-sharded over {world} GPU(s)" + (
+                                       f"; this line: rank {part_rank}'s strided shard of a {part_world}-rank job "
+                                       f"alone on one GPU (value = that rank's rate)" if args.shard_of else ""),
                        "photon_n_job": photon_n_job, "grid": f"{args.grid}x{args.grid}",
                        "superphotons_per_pass_rank0": n_rank // max(1, args.steps),
                        "bias_counters": bias_counters,
+                       "valid_for_parity": valid_for_parity,
+                       "peer_access": peer_matrix,
                        "parallelism": f"strided zone shards x{world}" + (
                            (", ranks sharing GPUs (rehearsal): passes stashed on the device, one gloo reduction per job"
                             if shared_gpu else ", passes stashed on the device, one RCCL all-reduce per job")

@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "../../include/grmonty_amd.h"
+#include "../../include/grmonty_amd_debug.h"
 
 namespace grm {
 
@@ -577,37 +578,12 @@ __device__ __forceinline__ double quad_pick(const double v[4], int q) {
     return (q & 2) ? hi : lo;
 }
 
-/* row q of the connection (harm_model.cpp:1436-1569) into L, from the shared products */
-__device__ __forceinline__ void connection_quad_row(const Params &P, const Trig &T, int q, double L[10]) {
-    ConnPre Q;
-    connection_pre(P, T, Q);
-    if (q == 0)
-        connection_row(Q, 0, L);
-    else if (q == 1)
-        connection_row(Q, 1, L);
-    else if (q == 2)
-        connection_row(Q, 2, L);
-    else
-        connection_row(Q, 3, L);
-}
-
 /* geo_rhs of one row (the same expression, harm_model.cpp:1255-1262) */
 __device__ __forceinline__ double geo_rhs_row(const double L[10], const double k[4]) {
     double d = -2.0 * (k[0] * (L[1] * k[1] + L[2] * k[2] + L[3] * k[3]) + k[1] * (L[5] * k[2] + L[6] * k[3]) +
                        L[8] * k[2] * k[3]);
     d -= (L[0] * k[0] * k[0] + L[4] * k[1] * k[1] + L[7] * k[2] * k[2] + L[9] * k[3] * k[3]);
     return d;
-}
-
-/* row q by selection from all four rows formed on every lane (full ILP, 60 selects) */
-__device__ __forceinline__ void connection_quad_sel(const Params &P, const Trig &T, int q, double L[10]) {
-    Conn C;
-    connection(P, T, C);
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-        const double v[4] = {C.c[0][j], C.c[1][j], C.c[2][j], C.c[3][j]};
-        L[j] = quad_pick(v, q);
-    }
 }
 
 /* row q from two exec-masked blocks of two rows each (lanes 0-1 form rows 0, 1; lanes 2-3 rows 2, 3):
@@ -628,20 +604,15 @@ __device__ __forceinline__ void connection_quad_half(const Params &P, const Trig
 }
 
 /* push_attempt on a quad (q = lane & 3; x, k, dk, e_0_s identical over the quad on entry and exit);
- * ROWS: how row q reaches lane q (0 divergent blocks, 1 selected from all four rows, 2 two blocks of two) */
-template <int ROWS = 0>
+ * row q of the connection reaches lane q from two exec-masked blocks of two rows each (four divergent
+ * one-row blocks and a 60-select pick from all four rows were measured slower: DESIGN.md §4.2) */
 __device__ __forceinline__ bool push_attempt_quad(const Params &P, double x[4], double k[4], double dk[4],
                                                   double e_0_s, double dl, double &e_1, Trig &T, Gcov &G, int q) {
     double kp[4];
     push_kick(x, k, dk, dl, kp);
     trig_at(P, x, T);
     double L[10];
-    if (ROWS == 0)
-        connection_quad_row(P, T, q, L);
-    else if (ROWS == 1)
-        connection_quad_sel(P, T, q, L);
-    else
-        connection_quad_half(P, T, q, L);
+    connection_quad_half(P, T, q, L);
     gcov_from_trig(P, T, G);
     const double dl_2 = 0.5 * dl;
     const double kq = quad_pick(k, q); /* the half-kicked k^q */

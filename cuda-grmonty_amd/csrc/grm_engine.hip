@@ -119,8 +119,6 @@ struct Ctl {
     int admit_slack;
     unsigned long long admit_b0; /* first batch */
     unsigned long long admit_spread; /* photons one wave claims at most per warm-up claim (0: no cap) */
-    unsigned warm_blocks, warm_waves; /* the waves that take the warm-up's batches: blockIdx < warm_blocks,
-                                       * wave-in-workgroup < warm_waves (the rest park) */
     unsigned long long *admit_end, *in_flight;
     unsigned long long *waves;  /* per-wave record of the launch: start, exit (s_memrealtime), trips, photons */
     unsigned long long *phases; /* s_memrealtime when the warm-up admission ended ([0]) and the pool's
@@ -137,7 +135,6 @@ struct Ctl {
     LoneRec *lone;
     unsigned long long lone_cap, *lone_count;
     int lone_all;
-    int lone_k; /* the pool drained and the stack empty, a wave with <= lone_k photons hands them all over */
     /* early hand-over of long photons to the concurrent early_kernel (early_q null = off): a photon
      * of >= early_steps steps at the top of a step; slots claimed by *early_tail, published by
      * early_ready[slot] = early_tag; *wg_exit counts exited workgroups, the last sets *early_done;
@@ -750,10 +747,6 @@ __device__ __forceinline__ double bcast(double v, int src) {
  * rank r (0 for the state's owner) attempts depth + r.  Leaves the completed push in every lane. */
 /* QUAD: the lone geometry wave's form -- quad r of lanes attempts depth + r with the quad-parallel
  * push (push_attempt_quad), rank = lane / 4 (16 ranks still cover every depth to MAX_SUBDIV) */
-/* how connection row q reaches lane q of the lone geometry wave's quads (push_attempt_quad): two
- * blocks of two rows (1.34-1.35 us/step on the long photon; selected from all four rows 1.37-1.38,
- * four divergent blocks 1.38-1.41, profiles/r03_ab/s3e_*, s3h_*) */
-constexpr int GEO_ROWS = 2;
 template <bool QUAD = false>
 __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[4], double dk[4], double &e_0_s,
                                          double hlen, int depth, uint32_t pend, int rank, int owner) {
@@ -768,7 +761,7 @@ __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[
             if (d <= MAX_SUBDIV) {
                 Trig T;
                 Gcov G;
-                const bool fail = QUAD ? push_attempt_quad<GEO_ROWS>(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G,
+                const bool fail = QUAD ? push_attempt_quad(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G,
                                                               (int)(threadIdx.x & 3))
                                        : push_attempt(P, x, k, dk, e_0_s, ldexp(hlen, -d), e_1, T, G);
                 ok = !fail || d == MAX_SUBDIV;
@@ -880,7 +873,6 @@ __device__ __forceinline__ void push_overflow(const Ctl &C, const double x[4], c
  * itself and restarts the geometry wave from it (a new generation; steps of the old one are
  * discarded by their tag).  Both halves of a step then run at once on two SIMDs. */
 constexpr int LONE_RING = 32, LONE_BATCH = 16;
-constexpr int LONE_K_MAX = 16; /* hand-overs per wave at the end of a launch (GRM_OPT_LONE_K) */
 constexpr unsigned long long LONE_STOP = ~0ull;
 struct alignas(16) LoneSlot {
     double out[13], dl;     /* the state after the push (x, k, dk/dlambda, e_0_s) and the step size */
@@ -1058,7 +1050,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
                     Trig T;
                     Gcov G;
                     /* every quad of lanes makes the attempt, lane q contracting connection row q */
-                    fail = GEO_QUAD ? push_attempt_quad<GEO_ROWS>(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
+                    fail = GEO_QUAD ? push_attempt_quad(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
                                     : push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
                     if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
 #pragma unroll
@@ -1921,7 +1913,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         const Ctl &C = karg_ctl(kt);
         ++wave_trips;
         TCOUNT(4);
-        if (warm && (blockIdx.x >= C.warm_blocks || (unsigned)wave >= C.warm_waves)) {
+        if (warm && blockIdx.x >= WARM_BLOCKS) {
             /* the warm-up's admission batches are small: the waves of the first WARM_BLOCKS
              * workgroups take them, the rest wait here without touching the counters (their polling
              * would contend with the warm-up's own counter traffic) until the admission is over */
@@ -2151,7 +2143,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             const unsigned long long act = __ballot(active);
             const int n_act = __popcll(act);
             const bool alone = n_act == 1 && *wtop == 0;
-            if (C.lone && ((n_act <= C.lone_k && *wtop == 0) || C.lone_all)) {
+            if (C.lone && (alone || C.lone_all)) {
                 /* a full hand-over queue is read, not claimed, and the photons stay in the lane loop
                  * (claiming past the cap and skipping the trip would retry forever) */
                 const bool hand = active && L.phase == 0 &&
@@ -2417,7 +2409,6 @@ struct grm_engine {
     LoneRec *d_lone = nullptr;             /* photons handed over to lone_kernel */
     unsigned long long lone_cap = 0;
     int lone = 1;                          /* GRM_OPT_LONE */
-    int lone_k = 1;                        /* GRM_OPT_LONE_K */
     /* early hand-over of long photons to early_kernel on a second stream (GRM_OPT_EARLY_STEPS) */
     int early_steps = 5000;
     bool early_serial = false; /* test: the worker ahead of the main launch on its stream */
@@ -2438,7 +2429,6 @@ struct grm_engine {
      * WARMUP_PHOTONS warm-up; none for the ramp to a grid of lanes (its batches outnumber the
      * warm-up's lanes) */
     int64_t warmup_spread = -1;
-    int64_t warmup_blocks = 0, warmup_waves = 0; /* GRM_OPT_WARMUP_BLOCKS / _WAVES (0 = default) */
     /* host-mapped control block: ctl_kernel mirrors the counters and the small words here (ctr,
      * small) and the emission scan writes its total (word[4]); the host reads them after a stream
      * synchronisation, so a pass runs without copy or fill kernels (see ctl_kernel) */
@@ -2524,7 +2514,7 @@ int alloc_lanes(grm_engine *e) {
          * mode GRM_OPT_LONE = 2, sized in run_passes) */
         if (e->d_lone) (void)hipFree(e->d_lone);
         e->d_lone = nullptr;
-        e->lone_cap = lanes / 64 * LONE_K_MAX;
+        e->lone_cap = lanes / 64;
         HIPCHK(e, hipMalloc(&e->d_lone, e->lone_cap * sizeof(LoneRec)));
         e->lanes = lanes;
     }
@@ -2614,7 +2604,6 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.lone_cap = e->lone_cap;
     C.lone_count = e->d_small + 7;
     C.lone_all = e->lone == 2;
-    C.lone_k = e->lone_k;
     C.karg_test = e->karg_test;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
@@ -2631,8 +2620,6 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.admit_b0 = e->warmup_b0;
         C.admit_spread = e->warmup_spread >= 0 ? (unsigned long long)e->warmup_spread
                                                : (e->warmup == -2 && small ? 0ull : WARMUP_SPREAD);
-        C.warm_blocks = e->warmup_blocks > 0 ? (unsigned)e->warmup_blocks : WARM_BLOCKS;
-        C.warm_waves = e->warmup_waves > 0 ? (unsigned)e->warmup_waves : (unsigned)(BLOCK / 64);
     }
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
@@ -3029,12 +3016,9 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_LONE: e->lone = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_WARMUP_BATCH: e->warmup_b0 = v < 1 ? 1 : (unsigned long long)v; return 0;
     case GRM_OPT_WARMUP_SPREAD: e->warmup_spread = v < 0 ? -1 : v; return 0;
-    case GRM_OPT_WARMUP_BLOCKS: e->warmup_blocks = v < 0 ? 0 : v; return 0;
-    case GRM_OPT_WARMUP_WAVES: e->warmup_waves = v < 0 ? 0 : (v > BLOCK / 64 ? BLOCK / 64 : v); return 0;
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
-    case GRM_OPT_LONE_K: e->lone_k = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
     default: e->err = "unknown option"; return -1;
     }
@@ -3506,10 +3490,10 @@ int grm_engine_stash(grm_engine *e, int slot) {
     return 0;
 }
 
-int grm_engine_allreduce_stash(grm_engine *e, int n_slots) {
+int grm_engine_allreduce_stash(grm_engine *e, int first, int n_slots) {
     if (!e) return -1;
-    if (n_slots < 0 || n_slots > e->stash_cap) {
-        e->err = "grm_engine_allreduce_stash: bad slot count";
+    if (first < 0 || n_slots < 0 || first + n_slots > e->stash_cap) {
+        e->err = "grm_engine_allreduce_stash: slots outside the reserved stash";
         return -1;
     }
     if (!e->comm) {
@@ -3521,14 +3505,14 @@ int grm_engine_allreduce_stash(grm_engine *e, int n_slots) {
     const size_t ncell = (size_t)N_TH_BINS * N_E_BINS * (sizeof(grm_spectrum_cell) / sizeof(double));
     ncclResult_t r = ncclGroupStart();
     if (r == ncclSuccess)
-        r = ncclAllReduce(e->d_stash_spec, e->d_stash_spec, (size_t)n_slots * ncell, ncclFloat64, ncclSum, e->comm,
-                          e->stream);
+        r = ncclAllReduce(e->d_stash_spec + (size_t)first * ncell, e->d_stash_spec + (size_t)first * ncell,
+                          (size_t)n_slots * ncell, ncclFloat64, ncclSum, e->comm, e->stream);
     if (r == ncclSuccess)
-        r = ncclAllReduce(e->d_stash_sum, e->d_stash_sum, (size_t)n_slots * STASH_SUMS, ncclUint64, ncclSum, e->comm,
-                          e->stream);
+        r = ncclAllReduce(e->d_stash_sum + (size_t)first * STASH_SUMS, e->d_stash_sum + (size_t)first * STASH_SUMS,
+                          (size_t)n_slots * STASH_SUMS, ncclUint64, ncclSum, e->comm, e->stream);
     if (r == ncclSuccess)
-        r = ncclAllReduce(e->d_stash_max, e->d_stash_max, (size_t)n_slots * STASH_MAXS, ncclUint64, ncclMax, e->comm,
-                          e->stream);
+        r = ncclAllReduce(e->d_stash_max + (size_t)first * STASH_MAXS, e->d_stash_max + (size_t)first * STASH_MAXS,
+                          (size_t)n_slots * STASH_MAXS, ncclUint64, ncclMax, e->comm, e->stream);
     const ncclResult_t r2 = ncclGroupEnd();
     if (r == ncclSuccess) r = r2;
     if (r != ncclSuccess) {

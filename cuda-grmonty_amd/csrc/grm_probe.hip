@@ -61,7 +61,7 @@ __global__ void probe_kernel(Params P, int which, const double *in, int is, doub
         Trig T;
         Gcov G;
         const bool f = push_attempt(P, x, k, dk, a[12], a[13], e1, T, G);
-        const bool fq = push_attempt_quad<2>(P, xq, kq, dkq, a[12], a[13], e1q, T, G, q); /* the lone default */
+        const bool fq = push_attempt_quad(P, xq, kq, dkq, a[12], a[13], e1q, T, G, q); /* the lone default */
         if (q == 0) {
             for (int i = 0; i < 4; ++i) {
                 store(o, i, x[i]);

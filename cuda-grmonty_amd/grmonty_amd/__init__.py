@@ -25,6 +25,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GRMONTY_AMD_LIB") or os.path.join(PKG_DIR, "libgrmonty_amd.so")
 REPO_DIR = os.path.dirname(PKG_DIR)
 HEADER_PATH = os.path.join(REPO_DIR, "include", "grmonty_amd.h")
+DEBUG_HEADER_PATH = os.path.join(REPO_DIR, "include", "grmonty_amd_debug.h")
 
 DP = C.POINTER(C.c_double)
 VP = C.c_void_p
@@ -53,10 +54,7 @@ OPT_WARMUP_BATCH = 14
 OPT_EARLY_STEPS = 15
 OPT_EARLY_SERIAL = 16
 OPT_KARG_TEST = 17
-OPT_LONE_K = 18
 OPT_WARMUP_SPREAD = 19
-OPT_WARMUP_BLOCKS = 20
-OPT_WARMUP_WAVES = 21
 N_TH_BINS, N_E_BINS = 6, 200
 
 
@@ -133,7 +131,7 @@ SIGNATURES = {
     "grm_engine_allreduce": (C.c_int, [VP]),
     "grm_engine_stash_reserve": (C.c_int, [VP, C.c_int]),
     "grm_engine_stash": (C.c_int, [VP, C.c_int]),
-    "grm_engine_allreduce_stash": (C.c_int, [VP, C.c_int]),
+    "grm_engine_allreduce_stash": (C.c_int, [VP, C.c_int, C.c_int]),
     "grm_engine_stash_read": (C.c_int, [VP, C.c_int, VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "grm_engine_stash_raw": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, VP, C.c_int]),
@@ -446,8 +444,9 @@ class Engine:
     def stash(self, slot: int):
         self._check(self.L.grm_engine_stash(self.h, int(slot)))
 
-    def allreduce_stash(self, n_slots: int):
-        self._check(self.L.grm_engine_allreduce_stash(self.h, int(n_slots)))
+    def allreduce_stash(self, n_slots: int, first: int = 0):
+        """one grouped RCCL all-reduce of stash slots [first, first + n_slots)"""
+        self._check(self.L.grm_engine_allreduce_stash(self.h, int(first), int(n_slots)))
 
     def stash_read(self, slot: int):
         """(spectrum, n_recorded, n_scatt, max_tau_scatt, n_steps) of a stashed pass"""
@@ -555,9 +554,12 @@ def rccl_unique_id() -> bytes:
     return bytes(buf)
 
 
-def header_symbols(path: str = HEADER_PATH) -> list[str]:
-    """Names of the functions declared in the public C header (for the ABI test)."""
+def header_symbols(paths=(HEADER_PATH, DEBUG_HEADER_PATH)) -> list[str]:
+    """Names of the functions declared in the C headers -- the boundary (include/grmonty_amd.h) and
+    the diagnostic / probe entry points (include/grmonty_amd_debug.h) -- for the ABI test."""
     import re
-    txt = open(path).read()
+    if isinstance(paths, str):
+        paths = (paths,)
+    txt = "\n".join(open(p).read() for p in paths)
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(grm_[a-z0-9_]+)\s*\(", txt)))

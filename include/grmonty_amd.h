@@ -175,19 +175,12 @@ enum {
     /* test only: != 0 makes the transport kernel's kernel-argument check fail (the failure path must
      * end the call with an error, no photon tracked) */
     GRM_OPT_KARG_TEST = 17,
-    /* with GRM_OPT_LONE = 1: once the pool is drained, a wave whose stack is empty and that holds at
-     * most this many photons (1..64, default 1) hands them all to two-wave pairs of the lone kernel
-     * instead of stepping them in a nearly empty lane loop */
-    GRM_OPT_LONE_K = 18,
+    /* 18: retired (GRM_OPT_LONE_K, an experiment of round 3: no gain) */
     /* a wave claims at most this many photons of a warm-up admission batch at a time, spreading the
      * batch, and its photons' scattering families, over more waves (0: as many lanes as it has idle;
      * -1, the default: 4 in the 4,096-photon warm-up, 0 in the ramp of a small pass) */
-    GRM_OPT_WARMUP_SPREAD = 19,
-    /* the waves that take the warm-up's admission batches (the others park until it is over):
-     * the first this-many workgroups (0 or default: 64; larger values are capped at the grid) ... */
-    GRM_OPT_WARMUP_BLOCKS = 20,
-    /* ... and of each, its first this-many waves (1..8; 0 or default: all 8) */
-    GRM_OPT_WARMUP_WAVES = 21
+    GRM_OPT_WARMUP_SPREAD = 19
+    /* 20, 21: retired (GRM_OPT_WARMUP_BLOCKS / _WAVES, experiments of round 3: no gain) */
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
@@ -221,29 +214,8 @@ int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap);
  * valid for grm_engine_track_device until the next upload or destroy. */
 int grm_engine_upload(grm_engine *e, const grm_init_photon *batch, size_t n, grm_init_photon **dev_out);
 
-/* diagnostic: per-region wave cycles of a -DGRM_TIMING build, 48 slots (returns 1 if the build
- * is instrumented, 0 if not; out[] then stays zero) */
-int grm_engine_debug_timing(grm_engine *e, uint64_t out[48], int reset);
-
-/* diagnostic: per-wave record of the last transport launch, 4 x u64 per wave: start and exit
- * (s_memrealtime, 100 MHz), loop trips, superphotons tracked.  out holds cap waves; returns the
- * number of waves of the grid (-1 before the first launch). */
-int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap);
-
-/* diagnostic: state of the photons the watchdog abandoned, 16 doubles each: id, n_step, phase, depth,
- * pend, w, e_0_s, dl, x[4], k[4].  out holds cap records; returns the records kept (<= 256). */
-int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap);
-/* raw device counters: n_recorded, n_scatt, max_tau_scatt bits, n_steps, n_tracked, n_children,
- * n_overflow, n_dropped, n_primaries, max photon steps, lives > 1e5 steps, n_abandoned, abort, n_nan,
- * waves whose kernel-argument check failed, 1 reserved */
-int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]);
-/* diagnostic: the phases of the last call's main launch, s_memrealtime ticks (100 MHz): first wave
- * start, end of the live-bias warm-up admission (0 = none), the pool's last claim chunk taken (0 =
- * not reached), last wave exit */
-int grm_engine_debug_phases(grm_engine *e, uint64_t out[4]);
-/* the live-bias warm-up's admission log of the same launch: out[2i] = s_memrealtime tick when batch
- * i + 1 opened, out[2i + 1] = photons in flight then (i < cap); returns the number of openings */
-int64_t grm_engine_debug_admissions(grm_engine *e, uint64_t *out, size_t cap);
+/* diagnostics (per-wave records, timing builds, watchdog records, raw counters) and the
+ * per-function device probes of the parity tests: include/grmonty_amd_debug.h */
 
 /* --- multi-GPU: one engine per GPU/process, RCCL over xGMI ------------------------------ */
 /* rank 0 creates the 128-byte RCCL unique id and ships it to the others (any transport) */
@@ -261,7 +233,9 @@ int grm_engine_allreduce(grm_engine *e);
  * others at that pass).  Same reduction as grm_engine_allreduce (harm_model.cpp:340-414 is one pass). */
 int grm_engine_stash_reserve(grm_engine *e, int n_slots);
 int grm_engine_stash(grm_engine *e, int slot);
-int grm_engine_allreduce_stash(grm_engine *e, int n_slots);
+/* slots [first, first + n_slots): a job reduces its warm-up slots and its timed slots separately,
+ * each once (re-reducing a slot would multiply it by the rank count) */
+int grm_engine_allreduce_stash(grm_engine *e, int first, int n_slots);
 int grm_engine_stash_read(grm_engine *e, int slot, grm_spectrum_cell *spec, uint64_t *n_rec, uint64_t *n_scatt,
                           double *max_tau, uint64_t *n_steps);
 /* The stash's raw words of slots [first, first + n_slots), in the engine's own packing, read
@@ -376,11 +350,6 @@ int grm_write_spectrum(const grm_model *m, const grm_spectrum_cell *spectrum, co
  * log10(E) then, per theta bin, nph (recorded superphotons), dn_dle (sum w) and de_dle (sum w E),
  * "%.17g" -- what an effective-N / KS comparison of two spectra needs and the 37-column file lacks. */
 int grm_write_spectrum_stats(const grm_model *m, const grm_spectrum_cell *spectrum, const char *path);
-
-/* --- per-function device probes (parity tests; one lane per input) --------------------- */
-/* which: see GRM_PROBE_* in DESIGN.md / csrc/grm_probe.hip. in/out are host arrays of
- * n * in_stride / n * out_stride doubles. */
-int grm_probe(grm_engine *e, int which, const double *in, int in_stride, double *out, int out_stride, size_t n);
 
 /* ABI introspection: sizes of the POD structs (0 header 1 units 2 init_photon 3 spectrum_cell
  * 4 trace 5 stats 6 emit_zone) */

@@ -151,7 +151,6 @@ static inline uint64_t child_id(uint64_t parent_id, uint64_t parent_ctr) {
 struct Rng {
     int mode = GRMO_RNG_MT19937;
     std::mt19937 *mt = nullptr; /* shared stream (reference semantics) */
-    std::mt19937 own;
     uint32_t key[2] = {0, 0};
     uint64_t id = 0, ctr = 0;
 
@@ -1891,6 +1890,369 @@ int64_t grmo_track_batch(grmo_model *m, const grmo_init_photon *ph, size_t n, in
     m->bias_mode = GRMO_BIAS_LIVE;
     return m->trace_n;
 }
+
+} /* extern "C" (the emulator's helpers below are C++) */
+
+/* ------------------------------------------------------------------------- */
+/* Concurrency emulator (test infrastructure): track_super_photon            */
+/* (harm_model.cpp:894-1069) cut at its loop boundary, so that W photons can  */
+/* be advanced round-robin one loop iteration at a time with bias_func        */
+/* (:1391-1404) reading counter snapshots that lag the records (:1296-1298,   */
+/* :1319-1320) -- the way the device's persistent lanes see them.  With one   */
+/* slot, depth-first children (:1023) and a snapshot per round it is the      */
+/* serial reference, operation for operation (tests/test_oracle_concurrent).  */
+/* ------------------------------------------------------------------------- */
+namespace grmo {
+namespace {
+
+/* one photon in flight: track_super_photon's loop locals */
+struct Flight {
+    Photon ph;
+    Rng rng;
+    Fluid fp; /* the last fluid evaluation: fp.n_e gates the next interaction (:937); a scattering
+               * parent's continuation (:1026-1039) reads it */
+    double alpha_scatti = 0, alpha_absi = 0, bi = 0;
+    double pend_dta = 0, pend_dts = 0; /* the scattering step's optical depths, added after the child (:1054-1055) */
+    int n_step = 0;
+    int phase = 0; /* 0 set-up pending (:895-917), 1 in the loop, 2 resume after a depth-first child */
+};
+
+enum { FL_GO = 0, FL_END = 1, FL_CHILD = 2 };
+
+/* the loop's exit (:1064-1068) */
+static void flight_finish(grmo_model *m, Flight &f, int reason) {
+    if (f.ph.x[1] > D.x1_max && f.n_step <= MAX_N_STEP) {
+        int ix2, ie;
+        const bool binned = record_super_photon(m, f.ph, ix2, ie);
+        emit_trace(m, f.ph, f.n_step, binned ? 0 : 1, ix2, ie);
+    } else {
+        emit_trace(m, f.ph, f.n_step, reason, -1, -1);
+    }
+}
+
+/* :895-917 */
+static int flight_setup(grmo_model *m, Flight &f) {
+    Photon &ph = f.ph;
+    if (std::isnan(ph.x[0]) || std::isnan(ph.x[1]) || std::isnan(ph.x[2]) || std::isnan(ph.x[3]) ||
+        std::isnan(ph.k[0]) || std::isnan(ph.k[1]) || std::isnan(ph.k[2]) || std::isnan(ph.k[3]) || ph.w == 0.0) {
+        emit_trace(m, ph, 0, 4, -1, -1);
+        return FL_END;
+    }
+    double g[4][4];
+    gcov_func(m, ph.x, g);
+    fluid_params(m, ph.x, g, f.fp);
+    const double theta = bk_angle(ph.k, f.fp.u_cov, f.fp.b_cov, f.fp.b, m->units.b_unit);
+    const double nu = fluid_nu(ph.k, f.fp.u_cov);
+    f.alpha_scatti = alpha_inv_scatt(m, nu, f.fp.theta_e, f.fp.n_e);
+    f.alpha_absi = alpha_inv_abs(m, nu, f.fp.theta_e, f.fp.n_e, f.fp.b, theta);
+    f.bi = bias_func(m, f.fp.theta_e, ph.w);
+    init_dkdlam(m, ph.x, ph.k, ph.dkdlam);
+    f.n_step = 0;
+    f.phase = 1;
+    return FL_GO;
+}
+
+/* the scattering parent's continuation at the scattering point (:1026-1039) */
+static void flight_continue(grmo_model *m, Flight &f) {
+    Photon &ph = f.ph;
+    const Fluid &fp = f.fp;
+    const double theta = bk_angle(ph.k, fp.u_cov, fp.b_cov, fp.b, m->units.b_unit);
+    const double nu = fluid_nu(ph.k, fp.u_cov);
+    if (nu < 0.0) {
+        f.alpha_scatti = 0.0;
+        f.alpha_absi = 0.0;
+    } else {
+        f.alpha_scatti = alpha_inv_scatt(m, nu, fp.theta_e, fp.n_e);
+        f.alpha_absi = alpha_inv_abs(m, nu, fp.theta_e, fp.n_e, fp.b, theta);
+    }
+    f.bi = bias_func(m, fp.theta_e, ph.w);
+}
+
+/* the loop's tail (:1054-1063): optical depths, step count */
+static int flight_tail(grmo_model *m, Flight &f, double d_tau_abs, double d_tau_scatt) {
+    f.ph.tau_abs += d_tau_abs;
+    f.ph.tau_scatt += d_tau_scatt;
+    ++f.n_step;
+    if (f.n_step > MAX_N_STEP) {
+        flight_finish(m, f, 3);
+        return FL_END;
+    }
+    return FL_GO;
+}
+
+/* one iteration of the while loop (:919-1063), Philox streams.  A valid scattered child is
+ * returned in `child` (phase 0, its stream after the sampling, as :1023 hands it on): with
+ * depth_first the parent stops before its continuation (phase 2, resumed by flight_resume after
+ * the child has ended, as the recursion does); otherwise it continues at once (the device). */
+static int flight_step(grmo_model *m, uint64_t seed, Flight &f, Flight &child, bool depth_first) {
+    Photon &ph = f.ph;
+    Rng &rng = f.rng;
+    if (stop_criterion(m, ph, rng)) {
+        flight_finish(m, f, 2);
+        return FL_END;
+    }
+    double x2[4], k2[4], dk2[4], e0s2 = ph.e_0_s;
+    for (int i = 0; i < 4; ++i) {
+        x2[i] = ph.x[i];
+        k2[i] = ph.k[i];
+        dk2[i] = ph.dkdlam[i];
+    }
+    const double dl = step_size(m, ph.x, ph.k);
+    push_photon(m, ph.x, ph.k, ph.dkdlam, ph.e_0_s, dl, 0);
+    m->n_steps++;
+    if (stop_criterion(m, ph, rng)) {
+        flight_finish(m, f, 2);
+        return FL_END;
+    }
+    if (!(f.alpha_absi > 0.0 || f.alpha_scatti > 0.0 || f.fp.n_e > 0.0)) return flight_tail(m, f, 0.0, 0.0) == FL_END ? FL_END : FL_GO;
+    double g[4][4];
+    gcov_func(m, ph.x, g);
+    Fluid &fp = f.fp;
+    fluid_params(m, ph.x, g, fp);
+    const bool bound_flag = fp.n_e == 0.0;
+    double theta = 0.0, nu = 0.0;
+    if (!bound_flag) {
+        theta = bk_angle(ph.k, fp.u_cov, fp.b_cov, fp.b, m->units.b_unit);
+        nu = fluid_nu(ph.k, fp.u_cov);
+    }
+    double d_tau_scatt, d_tau_abs, bias;
+    if (bound_flag || nu < 0.0) {
+        d_tau_scatt = 0.5 * f.alpha_scatti * m->d_tau_k * dl;
+        d_tau_abs = 0.5 * f.alpha_absi * m->d_tau_k * dl;
+        f.alpha_scatti = 0.0;
+        f.alpha_absi = 0.0;
+        bias = 0.0;
+        f.bi = 0.0;
+    } else {
+        const double alpha_scattf = alpha_inv_scatt(m, nu, fp.theta_e, fp.n_e);
+        d_tau_scatt = 0.5 * (f.alpha_scatti + alpha_scattf) * m->d_tau_k * dl;
+        f.alpha_scatti = alpha_scattf;
+        const double alpha_absf = alpha_inv_abs(m, nu, fp.theta_e, fp.n_e, fp.b, theta);
+        d_tau_abs = 0.5 * (f.alpha_absi + alpha_absf) * m->d_tau_k * dl;
+        f.alpha_absi = alpha_absf;
+        const double bf = bias_func(m, fp.theta_e, ph.w);
+        bias = 0.5 * (f.bi + bf);
+        f.bi = bf;
+    }
+    const double x1 = -std::log(rng.uniform());
+    Photon pc;
+    std::memset(&pc, 0, sizeof(pc));
+    pc.w = ph.w / bias;
+    int ret = FL_GO;
+    if (bias * d_tau_scatt > x1 && pc.w > WEIGHT_MIN) {
+        const double frac = x1 / (bias * d_tau_scatt);
+        d_tau_abs *= frac;
+        if (d_tau_abs > 100) {
+            emit_trace(m, ph, f.n_step, 2, -1, -1);
+            return FL_END;
+        }
+        d_tau_scatt *= frac;
+        const double d_tau = d_tau_abs + d_tau_scatt;
+        if (d_tau_abs < 1.0e-3)
+            ph.w *= (1.0 - d_tau / 24.0 * (24.0 - d_tau * (12.0 - d_tau * (4.0 - d_tau))));
+        else
+            ph.w *= std::exp(-d_tau);
+        push_photon(m, x2, k2, dk2, e0s2, dl * frac, 0);
+        for (int i = 0; i < 4; ++i) {
+            ph.x[i] = x2[i];
+            ph.k[i] = k2[i];
+            ph.dkdlam[i] = dk2[i];
+        }
+        ph.e_0_s = e0s2;
+        gcov_func(m, ph.x, g);
+        fluid_params(m, ph.x, g, fp);
+        if (fp.n_e > 0.0) {
+            const uint64_t cid = child_id(ph.id, rng.ctr);
+            Rng crng = Rng::philox(seed, cid);
+            const int st = scatter_super_photon(m, ph, pc, fp, g, crng);
+            if (ph.w < 1.0e-100) {
+                emit_trace(m, ph, f.n_step, 2, -1, -1);
+                return FL_END;
+            }
+            pc.id = cid;
+            pc.parent_id = ph.id;
+            if (st == 0) {
+                child = Flight();
+                child.ph = pc;
+                child.rng = crng;
+                child.phase = 0;
+                ret = FL_CHILD;
+                if (depth_first) {
+                    f.pend_dta = d_tau_abs;
+                    f.pend_dts = d_tau_scatt;
+                    f.phase = 2;
+                    return FL_CHILD;
+                }
+            } else {
+                emit_trace(m, pc, 0, 4, -1, -1);
+            }
+        }
+        flight_continue(m, f);
+    } else {
+        if (d_tau_abs > 100) {
+            emit_trace(m, ph, f.n_step, 2, -1, -1);
+            return FL_END;
+        }
+        const double d_tau = d_tau_abs + d_tau_scatt;
+        if (d_tau < 1.0e-3)
+            ph.w *= (1. - d_tau / 24. * (24. - d_tau * (12. - d_tau * (4. - d_tau))));
+        else
+            ph.w *= std::exp(-d_tau);
+    }
+    if (flight_tail(m, f, d_tau_abs, d_tau_scatt) == FL_END) {
+        /* the parent ended at max_n_step; a child handed back with it is still tracked */
+        return ret == FL_CHILD ? FL_CHILD | 4 : FL_END;
+    }
+    return ret;
+}
+
+/* a depth-first parent after its child (:1024-1063) */
+static int flight_resume(grmo_model *m, Flight &f) {
+    flight_continue(m, f);
+    f.phase = 1;
+    return flight_tail(m, f, f.pend_dta, f.pend_dts);
+}
+
+} /* namespace */
+} /* namespace grmo */
+
+extern "C" {
+
+/* Track a batch of emitted photons the way a concurrent engine schedules them (see the block
+ * comment above and grmonty_oracle.h).  Philox streams only (id = id_base + batch index). */
+int64_t grmo_track_concurrent(grmo_model *m, const grmo_init_photon *batch, size_t n, uint64_t seed,
+                              uint64_t id_base, const int64_t *cfg_in, size_t n_cfg, grmo_trace *trace,
+                              size_t trace_cap, double *timeline, size_t timeline_cap, int64_t *n_timeline) {
+    using namespace grmo;
+    int64_t cfg[GRMO_EMU_NCFG] = {1, 1, 1, 1, 1, 0, 0, 4, 64, 0, 0};
+    for (size_t i = 0; i < n_cfg && i < GRMO_EMU_NCFG; ++i) cfg[i] = cfg_in[i];
+    const int64_t W = std::max<int64_t>(1, cfg[GRMO_EMU_SLOTS]);
+    const int64_t G = std::max<int64_t>(1, cfg[GRMO_EMU_GROUP]);
+    const int64_t R = std::max<int64_t>(1, cfg[GRMO_EMU_REFRESH]);
+    const size_t child_min = (size_t)std::max<int64_t>(1, cfg[GRMO_EMU_CHILD_MIN]);
+    const bool depth_first = cfg[GRMO_EMU_DEPTH_FIRST] != 0;
+    const int sh = cfg[GRMO_EMU_CLAIM_SH] >= 0 ? (int)cfg[GRMO_EMU_CLAIM_SH] : (n >= (2ull << 12) ? 12 : 0);
+    const uint64_t mm = (n + (1ull << sh) - 1) >> sh, n_pos = mm << sh;
+    const uint64_t warm_n = cfg[GRMO_EMU_WARM_N] < 0 ? (uint64_t)W : (uint64_t)cfg[GRMO_EMU_WARM_N];
+    const int warm_slack = (int)cfg[GRMO_EMU_WARM_SLACK];
+    const uint64_t warm_b0 = (uint64_t)std::max<int64_t>(1, cfg[GRMO_EMU_WARM_B0]);
+    const uint64_t cap_flight = cfg[GRMO_EMU_FLIGHT_CAP] > 0 ? (uint64_t)cfg[GRMO_EMU_FLIGHT_CAP] : ~0ull;
+    const int64_t tl_every = cfg[GRMO_EMU_TIMELINE];
+
+    m->bias_mode = GRMO_BIAS_FROZEN; /* bias_func reads the snapshot (b_scatt0, b_rec0, b_maxtau0) */
+    m->trace = trace;
+    m->trace_cap = trace ? trace_cap : 0;
+    m->trace_n = 0;
+    if (n_timeline) *n_timeline = 0;
+
+    std::vector<Flight> slot((size_t)W);
+    std::vector<char> busy((size_t)W, 0);
+    std::vector<std::vector<Flight>> parked((size_t)(depth_first ? W : 0)); /* suspended parents */
+    std::vector<std::vector<Flight>> stack((size_t)(depth_first ? 0 : (W + G - 1) / G)); /* deferred children */
+    uint64_t head = 0;             /* next claim position */
+    uint64_t admit_end = warm_n ? std::min<uint64_t>(warm_b0, std::min(warm_n, n_pos)) : ~0ull;
+    bool warm = warm_n != 0;
+    int64_t in_flight = 0;         /* photons started (primaries and children) and not ended */
+    uint64_t round = 0;
+    int64_t n_busy = 0;
+    size_t stacked = 0;
+    Flight child;
+    while (true) {
+        if (warm && head >= admit_end) {
+            if (admit_end >= std::min(warm_n, n_pos)) {
+                warm = false;
+                admit_end = ~0ull;
+            } else if ((uint64_t)in_flight <= (admit_end >> warm_slack)) {
+                const uint64_t h = admit_end;
+                admit_end = std::min(std::min(warm_n, n_pos), admit_end + std::max(warm_b0, std::min(h, warm_n - h)));
+            }
+        }
+        if (warm || round % (uint64_t)R == 0) {
+            m->b_scatt0 = m->n_scatt;
+            m->b_rec0 = m->n_recorded;
+            m->b_maxtau0 = m->max_tau_scatt;
+        }
+        if (tl_every > 0 && round % (uint64_t)tl_every == 0 && timeline && n_timeline &&
+            (size_t)(*n_timeline + 1) * 6 <= timeline_cap) {
+            double *t = timeline + 6 * (*n_timeline)++;
+            t[0] = (double)round;
+            t[1] = (double)head;
+            t[2] = (double)m->n_recorded;
+            t[3] = (double)m->n_scatt;
+            t[4] = m->max_tau_scatt;
+            t[5] = (double)in_flight;
+        }
+        const bool pool_done = head >= n_pos;
+        if (pool_done && n_busy == 0 && stacked == 0) break;
+        for (int64_t s = 0; s < W; ++s) {
+            Flight &f = slot[(size_t)s];
+            if (!busy[(size_t)s]) {
+                /* refill: a deferred child from the group's stack, else a primary */
+                bool got = false;
+                if (!depth_first) {
+                    std::vector<Flight> &st = stack[(size_t)(s / G)];
+                    const bool pool_open = head < n_pos && head < admit_end && (uint64_t)in_flight < cap_flight;
+                    if (!st.empty() && (st.size() >= child_min || !pool_open)) {
+                        f = st.back();
+                        st.pop_back();
+                        --stacked;
+                        got = true;
+                    }
+                }
+                while (!got && head < n_pos && head < admit_end && (uint64_t)in_flight < cap_flight) {
+                    const uint64_t q = head++;
+                    const uint64_t idx = (q & ((1ull << sh) - 1)) * mm + (q >> sh);
+                    if (idx >= n) continue; /* a hole of the interleave */
+                    f = Flight();
+                    f.ph = from_init(batch[idx]);
+                    f.ph.id = id_base + idx;
+                    f.ph.parent_id = ~0ull;
+                    f.rng = Rng::philox(seed, f.ph.id);
+                    ++m->n_created;
+                    ++in_flight;
+                    got = true;
+                }
+                if (!got) continue;
+                busy[(size_t)s] = 1;
+                ++n_busy;
+            }
+            int r;
+            if (f.phase == 0)
+                r = flight_setup(m, f);
+            else if (f.phase == 2)
+                r = flight_resume(m, f);
+            else
+                r = flight_step(m, seed, f, child, depth_first);
+            if (r & FL_CHILD) {
+                ++in_flight;
+                if (depth_first) {
+                    parked[(size_t)s].push_back(f);
+                    f = child;
+                    continue;
+                }
+                stack[(size_t)(s / G)].push_back(child);
+                ++stacked;
+                if (r == FL_CHILD) continue;
+            }
+            if (r != FL_GO) { /* ended */
+                --in_flight;
+                if (depth_first && !parked[(size_t)s].empty()) {
+                    f = parked[(size_t)s].back(); /* resumes next round, on the child's records */
+                    parked[(size_t)s].pop_back();
+                } else {
+                    busy[(size_t)s] = 0;
+                    --n_busy;
+                }
+            }
+        }
+        ++round;
+    }
+    m->trace = nullptr;
+    m->bias_mode = GRMO_BIAS_LIVE;
+    return (int64_t)round;
+}
+
+int64_t grmo_last_trace_count(const grmo_model *m) { return m->trace_n; }
 
 void grmo_reset_spectrum(grmo_model *m) {
     std::memset(m->spectrum, 0, sizeof(m->spectrum));

@@ -170,6 +170,35 @@ uint64_t grmo_child_id(uint64_t parent_id, uint64_t parent_ctr);
 int64_t grmo_track_batch(grmo_model *m, const grmo_init_photon *ph, size_t n, int rng_mode, uint64_t seed,
                          uint64_t id_base, int bias_mode, uint64_t scatt0, uint64_t rec0, double max_tau0,
                          grmo_trace *trace, size_t trace_cap);
+/* Concurrency emulator: the batch tracked as a concurrent engine schedules it -- `slots` photons
+ * advanced round-robin one loop iteration (harm_model.cpp:919-1063) per round, bias_func reading
+ * counter snapshots taken every `refresh` rounds, children either tracked depth-first in their
+ * parent's slot (the reference recursion, :1023) or deferred to a LIFO stack shared by `group`
+ * slots (the device's wave stacks), primaries claimed in the device's interleaved order
+ * (claim_sh: 2^sh runs; -1 = the engine's rule) under its warm-up admission (warm_n photons in
+ * batches b0, b0, 2 b0, ... each opened when in flight <= admitted >> slack; warm_n -1 = slots)
+ * and an optional cap on photons in flight.  Philox streams (id = id_base + index).  One slot,
+ * depth-first, refresh 1 is the serial reference operation for operation.  timeline (6 doubles
+ * per row: round, claims, recorded, scattered, max tau_scatt, in flight) every `timeline` rounds.
+ * Returns the number of rounds. */
+enum {
+    GRMO_EMU_SLOTS = 0,
+    GRMO_EMU_GROUP = 1,
+    GRMO_EMU_REFRESH = 2,
+    GRMO_EMU_CHILD_MIN = 3,
+    GRMO_EMU_DEPTH_FIRST = 4,
+    GRMO_EMU_CLAIM_SH = 5,
+    GRMO_EMU_WARM_N = 6,
+    GRMO_EMU_WARM_SLACK = 7,
+    GRMO_EMU_WARM_B0 = 8,
+    GRMO_EMU_FLIGHT_CAP = 9,
+    GRMO_EMU_TIMELINE = 10,
+    GRMO_EMU_NCFG = 11
+};
+int64_t grmo_track_concurrent(grmo_model *m, const grmo_init_photon *batch, size_t n, uint64_t seed,
+                              uint64_t id_base, const int64_t *cfg, size_t n_cfg, grmo_trace *trace,
+                              size_t trace_cap, double *timeline, size_t timeline_cap, int64_t *n_timeline);
+int64_t grmo_last_trace_count(const grmo_model *m); /* trace records the last traced call produced */
 void grmo_reset_spectrum(grmo_model *m);
 void grmo_set_spectrum(grmo_model *m, const grmo_spectrum in[6 * 200]);
 void grmo_get_spectrum(const grmo_model *m, grmo_spectrum out[6 * 200]);

@@ -111,6 +111,10 @@ def lib():
             "grmo_child_id": (C.c_uint64, [C.c_uint64, C.c_uint64]),
             "grmo_track_batch": (C.c_int64, [vp, vp, C.c_size_t, C.c_int, C.c_uint64, C.c_uint64, C.c_int,
                                              C.c_uint64, C.c_uint64, C.c_double, vp, C.c_size_t]),
+            "grmo_track_concurrent": (C.c_int64, [vp, vp, C.c_size_t, C.c_uint64, C.c_uint64,
+                                                  C.POINTER(C.c_int64), C.c_size_t, vp, C.c_size_t, DP,
+                                                  C.c_size_t, C.POINTER(C.c_int64)]),
+            "grmo_last_trace_count": (C.c_int64, [vp]),
             "grmo_reset_spectrum": (None, [vp]),
             "grmo_get_spectrum": (None, [vp, vp]),
             "grmo_set_spectrum": (None, [vp, vp]),
@@ -255,6 +259,33 @@ class OracleModel:
                                     1 if frozen else 0, scatt0, rec0, max_tau0,
                                     tr.ctypes.data_as(C.c_void_p) if trace_cap else None, trace_cap)
         return tr[:min(n, trace_cap)] if trace_cap else None
+
+    EMU_KEYS = ("slots", "group", "refresh", "child_min", "depth_first", "claim_sh", "warm_n", "warm_slack",
+                "warm_b0", "flight_cap", "timeline")
+    EMU_DEVICE = dict(slots=131072, group=64, refresh=64, child_min=8, depth_first=0, claim_sh=-1, warm_n=-1,
+                      warm_slack=4, warm_b0=64, flight_cap=0, timeline=0)
+    EMU_SERIAL = dict(slots=1, group=1, refresh=1, child_min=1, depth_first=1, claim_sh=0, warm_n=0,
+                      warm_slack=4, warm_b0=64, flight_cap=0, timeline=0)
+
+    def track_concurrent(self, photons: np.ndarray, seed: int = 123, id_base: int = 0, trace_cap: int = 0,
+                         timeline_cap: int = 0, **cfg):
+        """grmo_track_concurrent: the batch scheduled as a concurrent engine would (EMU_KEYS; defaults
+        EMU_SERIAL, i.e. the serial reference).  Returns (rounds, trace or None, timeline rows)."""
+        c = dict(self.EMU_SERIAL)
+        for k, v in cfg.items():
+            if k not in c:
+                raise KeyError(k)
+            c[k] = v
+        arr = (C.c_int64 * len(self.EMU_KEYS))(*[int(c[k]) for k in self.EMU_KEYS])
+        ph = np.ascontiguousarray(photons, dtype=INIT_PHOTON)
+        tr = np.zeros(max(trace_cap, 1), dtype=TRACE)
+        tl = np.zeros(max(timeline_cap, 1) * 6)
+        ntl = C.c_int64(0)
+        rounds = self.L.grmo_track_concurrent(self.h, ph.ctypes.data_as(C.c_void_p), len(ph), seed, id_base, arr,
+                                              len(self.EMU_KEYS), tr.ctypes.data_as(C.c_void_p) if trace_cap else None,
+                                              trace_cap, ptr(tl), len(tl), C.byref(ntl))
+        nt = min(self.L.grmo_last_trace_count(self.h), trace_cap)
+        return rounds, (tr[:nt] if trace_cap else None), tl[:6 * ntl.value].reshape(-1, 6)
 
     def spectrum(self) -> np.ndarray:
         s = np.zeros(6 * 200, dtype=SPECTRUM_CELL)

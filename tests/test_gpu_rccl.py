@@ -39,7 +39,8 @@ def test_single_rank_stash_reduce_is_identity(model64):
         e.track_device(d, len(ph))
         e.stash(slot)
         ref.append(e.finish())
-    e.allreduce_stash(3)
+    e.allreduce_stash(2, 1)  # slots [1, 3), then slot 0: each slot reduced once
+    e.allreduce_stash(1, 0)
     for slot, (s0, r0, c0, m0) in enumerate(ref):
         s1, r1, c1, m1, _ = e.stash_read(slot)
         assert (r0, c0, m0) == (r1, c1, m1)
