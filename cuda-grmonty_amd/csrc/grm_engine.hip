@@ -47,9 +47,9 @@ namespace {
 constexpr int BLOCK = GRM_BLOCK;
 constexpr int MIN_WAVES_PER_SIMD = BLOCK / 256;
 constexpr int STACK_DEPTH = 16;                 /* scatter-request slots per lane ... */
-constexpr int WSTACK_CAP = 64 * STACK_DEPTH;    /* ... pooled into one stack per wave (208 KB of HBM) */
+constexpr int WSTACK_CAP = 64 * STACK_DEPTH;    /* ... pooled into one stack per wave (192 KB of HBM) */
 
-/* 208-B scatter request: the state at a scattering event from which the child
+/* 192-B scatter request (three aligned 64-B segments per request): the state at a scattering event from which the child
  * photon is sampled later (scatter_super_photon, harm_model.cpp:1071-1145).
  * Lane stacks and overflow pools hold these. */
 struct alignas(16) SReq {
@@ -57,20 +57,22 @@ struct alignas(16) SReq {
     double u_con[4], b_con[4];  /* fluid 4-velocity and b^mu there */
     double b, theta_e;          /* |B| (Gauss), Theta_e there */
     double w;                   /* child weight w_parent / bias */
-    double n_e_0, theta_e_0, e_0;
+    double n_e_0, theta_e_0;
     uint64_t id, parent;        /* child stream id, parent stream id */
     int32_t n_scatt, pad0;
-    double pad1;
 };
-static_assert(sizeof(SReq) == 208, "SReq layout");
+static_assert(sizeof(SReq) == 192, "SReq layout");
 
-/* 80-B per-lane cold photon fields (touched only at birth, scattering and recording) */
+/* 64-B per-lane cold photon fields (touched only at birth, scattering and recording): one aligned
+ * segment per write.  The Photon fields l and e_0 (photon.hpp:19-36) are carried by the reference
+ * but enter no result -- record_super_photon never accumulates e_0 and nothing reads l
+ * (harm_model.cpp:1291-1335) -- so the lanes do not carry them. */
 struct alignas(16) Cold {
-    double e, l, x1i, x2i, n_e_0, theta_e_0, b_0, e_0;
+    double e, x1i, x2i, n_e_0, theta_e_0, b_0;
     uint64_t parent;
     double pad;
 };
-static_assert(sizeof(Cold) == 80, "Cold layout");
+static_assert(sizeof(Cold) == 64, "Cold layout");
 
 struct DevCounters {
     unsigned long long n_recorded, n_scatt, max_tau_bits, n_steps;
@@ -481,9 +483,9 @@ __device__ __forceinline__ void flush_records(const Ctl &C) {
 /* emitted photon -> lane (harm_model.cpp:373-391) */
 __device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L, Cold *cold) {
     const double2 *s = reinterpret_cast<const double2 *>(reinterpret_cast<const grm_init_photon *>(C.pool) + idx);
-    double2 v[8];
+    double2 v[7]; /* x, k, w, e, l, n_e_0, theta_e_0, b_0 (e_0 and n_scatt = 0 are not needed) */
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = s[q];
+    for (int q = 0; q < 7; ++q) v[q] = s[q];
     L.x[0] = v[0].x; L.x[1] = v[0].y; L.x[2] = v[1].x; L.x[3] = v[1].y;
     L.k[0] = v[2].x; L.k[1] = v[2].y; L.k[2] = v[3].x; L.k[3] = v[3].y;
     L.w = v[4].x;
@@ -493,13 +495,11 @@ __device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L
     L.rng.ctr_hi = 0;
     Cold c;
     c.e = v[4].y;
-    c.l = v[5].x;
     c.x1i = L.x[1];
     c.x2i = L.x[2];
     c.n_e_0 = v[5].y;
     c.theta_e_0 = v[6].x;
     c.b_0 = v[6].y;
-    c.e_0 = v[7].x;
     c.parent = ~0ull;
     c.pad = 0.0;
     *cold = c;
@@ -522,10 +522,8 @@ __device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane 
     c.n_e_0 = R.n_e_0;
     c.theta_e_0 = R.theta_e_0;
     c.b_0 = R.b;
-    c.e_0 = R.e_0;
     c.parent = R.parent;
     c.e = 0.0;
-    c.l = 0.0;
     c.pad = 0.0;
     Trig T;
     trig_at(P, R.x, T);
@@ -557,18 +555,16 @@ __device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane 
         for (int i = 0; i < 4; ++i) L.k[i] = ec[0][i] * ktp[0] + ec[1][i] * ktp[1] + ec[2][i] * ktp[2] + ec[3][i] * ktp[3];
         ok = !isnan(L.k[1]);
         if (ok) {
-            /* e_cov^T (-k0', k1', k2', k3'): only components 0 and 3 are needed (e, l) */
+            /* e_cov^T (-k0', k1', k2', k3'): only component 0 is needed (e; l enters no result) */
             ktp[0] = -ktp[0];
-            double t0 = 0.0, t3 = 0.0;
+            double t0 = 0.0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 double el[4];
                 tetrad_cov_row(ec, G, j, el);
                 t0 += el[0] * ktp[j];
-                t3 += el[3] * ktp[j];
             }
             c.e = -t0;
-            c.l = t3;
         }
     }
     *cold = c;
@@ -579,14 +575,14 @@ __device__ __forceinline__ void load_sreq(const SReq *src, SReq &R) {
     const double2 *s = reinterpret_cast<const double2 *>(src);
     double2 *d = reinterpret_cast<double2 *>(&R);
 #pragma unroll
-    for (int q = 0; q < 13; ++q) d[q] = s[q];
+    for (int q = 0; q < 12; ++q) d[q] = s[q];
 }
 
 __device__ __forceinline__ void store_sreq(SReq *dst, const SReq &R) {
     const double2 *s = reinterpret_cast<const double2 *>(&R);
     double2 *d = reinterpret_cast<double2 *>(dst);
 #pragma unroll
-    for (int q = 0; q < 13; ++q) d[q] = s[q];
+    for (int q = 0; q < 12; ++q) d[q] = s[q];
 }
 
 /* the scatter request of a scattered photon's child (scatter_super_photon's inputs, :1071-1145) */
@@ -606,12 +602,10 @@ __device__ __forceinline__ void make_sreq(SReq &R, const double x[4], const doub
     R.w = wc;
     R.n_e_0 = cold->n_e_0;
     R.theta_e_0 = cold->theta_e_0;
-    R.e_0 = cold->e_0;
     R.id = child_id(rng.id, rng.ctr);
     R.parent = rng.id;
     R.n_scatt = n_scatt + 1;
     R.pad0 = 0;
-    R.pad1 = 0.0;
 }
 
 /* append to the overflow pool (tracked by the next launch) */
@@ -830,7 +824,7 @@ struct alignas(16) LoneRec {
     uint32_t ctr;
     int32_t n_step, n_scatt, pad;
 };
-static_assert(sizeof(LoneRec) == 272, "LoneRec layout");
+static_assert(sizeof(LoneRec) == 256, "LoneRec layout");
 
 __device__ __forceinline__ void export_lone(LoneRec *r, const Lane &L, const Cold *cold) {
     /* field by field (a LoneRec built in registers first would add 68 VGPRs at this point of the loop) */
@@ -847,7 +841,7 @@ __device__ __forceinline__ void export_lone(LoneRec *r, const Lane &L, const Col
     d[9] = make_double2(L.bi(), L.fl_ne());
     const double2 *c = reinterpret_cast<const double2 *>(cold);
 #pragma unroll
-    for (int q = 0; q < 5; ++q) d[10 + q] = c[q];
+    for (int q = 0; q < 4; ++q) d[10 + q] = c[q];
     r->id = L.rng.id;
     r->ctr = L.rng.ctr;
     r->n_step = L.n_step;
@@ -2617,7 +2611,12 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.admit_h0 = e->history;
         C.admit_lim = limit;
         C.admit_slack = e->warmup_slack >= 0 ? e->warmup_slack : (e->warmup == -2 && small ? 4 : WARMUP_SLACK_LARGE);
-        C.admit_b0 = e->warmup_b0;
+        /* With the job's counters (n_peers ranks), every rank ramps at once: its batches are 1/n_peers
+         * of a single GPU's, so that the JOB admits 64, 64, 128, ... photons against the job-wide
+         * history as one GPU does (each rank at full batches would start n_peers x 64 photons on the
+         * empty history, and so on at every doubling) */
+        C.admit_b0 = C.n_peers > 1 ? std::max<unsigned long long>(1ull, e->warmup_b0 / (unsigned long long)C.n_peers)
+                                   : e->warmup_b0;
         C.admit_spread = e->warmup_spread >= 0 ? (unsigned long long)e->warmup_spread
                                                : (e->warmup == -2 && small ? 0ull : WARMUP_SPREAD);
     }

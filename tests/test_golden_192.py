@@ -50,3 +50,20 @@ def test_fixture_consistency(G):
     spec = g["spectrum123"]  # [6, 200, 13]: nph field (index 2) of seed 123
     assert int(round(spec[:, :, 2].sum())) == s["runs"][0]["recorded"]
     np.testing.assert_allclose(spec[:, :, 1].reshape(-1), g["cells"][0][:, 3], rtol=1e-9)
+
+
+def test_lag_emulator_fixture():
+    """The concurrency emulator's runs (tests/golden/lag_emulator_synth192_pn1e5.json): the serial
+    setting -- the reference scheduled serially, on the device's emission and Philox streams -- and
+    the device-like setting both agree with the reference's own mt19937 runs within Z_MAX combined
+    standard errors on every counter: the RNG streams and the concurrent scheduling of the live bias
+    move the counters by ~1-2 %, well inside the device test's bar (tests/test_gpu_parity_192.py)."""
+    from spectrum_stats import welch_z
+    emu = json.load(open(os.path.join(HERE, "golden", "lag_emulator_synth192_pn1e5.json")))
+    ora = json.load(open(os.path.join(HERE, "golden", "oracle_synth192_pn1e5.json")))["runs"]
+    for cfg in ("serial", "device"):
+        runs = [r for r in emu["runs"] if r["config"] == cfg]
+        assert len(runs) >= 20
+        for k in ("recorded", "scattered", "steps", "luminosity"):
+            diff, se, z = welch_z([r[k] for r in runs], [r[k] for r in ora])
+            assert abs(z) < 4.5, (cfg, k, z)

@@ -7,13 +7,11 @@
    counter block, the blocks linked (grm_engine_link_peers: the kernels run bias_func on the job's
    counters, harm_model.cpp:1391-1404, as grm_engine_set_peers makes them do across GPUs).  The job's
    counters are tested against the oracle's mean over N_DEV seeds: the luminosity (the estimator is
-   unbiased whatever the bias) within Z_MAX combined standard errors; the counters the live bias
-   drives (recorded, scattered, steps) within Z_MAX SE plus LAG_ALLOW of the oracle's mean -- the
-   concurrency lag of the live bias (the counters trail the claims by the photons in flight, DESIGN.md
-   §9): measured +2.9 / +4.6 / +4.9 to +6.8 % recorded at 2 / 4 / 8 emulated ranks over this round's
-   sessions (a z of 3.0-4.7 at 8 ranks), so a bar of Z_MAX SE alone fails by chance; the sharding
-   faults this test exists for are +17 to +43 % (below); and every rank's view of the job counters
-   (the kernels' own summation path) must equal the sums of the ranks'.
+   unbiased whatever the bias) and the counters the live bias drives (recorded, scattered, steps)
+   within Z_MAX combined standard errors (no allowance: the sharding faults this test exists for
+   are +17 to +43 %, below, and the job's warm-up now ramps job-wide -- each rank admits 1/N of a
+   single GPU's batches, grm_engine.hip run_passes); and every rank's view of the job counters (the
+   kernels' own summation path) must equal the sums of the ranks'.
    Without the link each rank's bias runs on its own history, N times shorter: +18 / +30 / +35 %
    recorded at 2 / 4 / 8 ranks with strided shards (profiles/r03b_pytest_multirank_unshared.log),
    +17 / +30 / +43 % with contiguous ones (profiles/r03a_multirank_contiguous.log).
@@ -41,9 +39,8 @@ from spectrum_stats import welch_z
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden", "oracle_synth192_pn1e5")
-N_DEV = 16
+N_DEV = 40
 Z_MAX = 4.5
-LAG_ALLOW = 0.05  # of the oracle's mean, for the bias-driven counters (see the module docstring)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
@@ -65,11 +62,10 @@ def test_emulated_ranks_vs_oracle(dump_dir, tmp_path, world):
     for k in KEYS:
         dev = [j[k] for j in jobs]
         diff, se, z = welch_z(dev, o[k])
-        allow = 0.0 if k == "luminosity" else LAG_ALLOW * o[k].mean()
         print(f"{world} ranks {k:10s} device {np.mean(dev):.6g} +- {np.std(dev, ddof=1):.3g} ({len(dev)} jobs)  "
               f"oracle {o[k].mean():.6g} +- {o[k].std(ddof=1):.3g} ({len(o[k])} runs)  diff {diff / o[k].mean():+.2%} "
-              f"= {z:+.2f} SE (bar {Z_MAX} SE{f' + {LAG_ALLOW:.0%}' if allow else ''})")
-        if abs(diff) > Z_MAX * se + allow:
+              f"= {z:+.2f} SE (bar {Z_MAX} SE)")
+        if abs(z) > Z_MAX:
             bad.append((k, z))
     for j in jobs:
         for v in j["job_view"]:

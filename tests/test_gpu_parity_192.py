@@ -14,10 +14,13 @@ Asserted:
     other at 1e-3, tests/test_golden_192.py); the spectrum's own sums cross-check the trace;
   - N_DEV jobs of distinct seeds: the MEAN of recorded, scattered, transport steps and luminosity
     against the oracle runs' mean, |difference| <= Z_MAX combined standard errors (Welch: each side's
-    own sample variance over its own run count).  With 24 device and 12+ oracle runs the standard
-    error is ~1.6 % of recorded / scattered, so a systematic bias of the scattering or adaptive-bias
-    machinery of more than ~7 % fails (one run against 5 sigma of the spread, the round-2 test,
-    let ~25 % through).
+    own sample variance over its own run count).  The live adaptive bias makes the counters of one
+    run scatter by 4-6 % (sd) on either side, so the means need many runs: 96 device jobs (0.25 s
+    each) against 60 oracle runs give a combined standard error of ~0.8 % of recorded, and a
+    systematic offset of the scattering or adaptive-bias machinery above ~3.5 % fails.  Measured
+    (round 4, 24-run means): the device +0.0 to +4.3 %, the oracle's concurrency emulator scheduling
+    the reference like the device +2.9 % and serially +1.2 % (tools/lag_emulator.py,
+    tests/golden/lag_emulator_synth192_pn1e5.json) -- concurrency moves the counters by ~1-2 %.
 """
 import json
 import os
@@ -31,7 +34,7 @@ from spectrum_stats import binned_ks, ks_crit, welch_z
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 G = os.path.join(HERE, "golden", "oracle_synth192_pn1e5")
-N_DEV = 24
+N_DEV = 96
 Z_MAX = 4.5
 
 
