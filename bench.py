@@ -27,7 +27,10 @@ over the N ranks, rank r taking every N-th zone from zone r (grmonty_amd.zone_sh
 rank's adaptive bias then sees a history of the whole disk; contiguous ranges moved the counters by
 +17..+43 %); --scaling strong: the job is photon_n, zone-sharded the same way.  Zone
 emission streams are keyed by zone and photon ids are global (rank r's id base = the photons of the
-ranks before it), so the union of the shards is exactly the single-GPU job's photon set.  The only exchange is the end-of-pass RCCL
+ranks before it), so the union of the shards' emitted photons is exactly the single-GPU job's set
+(the same initial states; a photon's transport stream is keyed by its id, which under strided shards
+is its rank-major position, not its single-GPU zone-order index -- so the N-rank job is an equally
+valid run with other transport draws, not a bit-replay of the single-GPU one).  The only exchange is the end-of-pass RCCL
 all-reduce (xGMI) of the 6x200x13 fp64 spectrum + counters, one communicator per rank, issued by the
 engine's C library on its stream.  torch.distributed runs with the gloo backend only (rendezvous,
 RCCL unique-id broadcast, barriers, max-over-ranks timing): torch's own HIP runtime is never

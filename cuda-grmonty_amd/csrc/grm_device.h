@@ -490,13 +490,16 @@ __device__ __forceinline__ void init_dkdlam(const Params &P, const double x[4], 
 
 /* harm_model.cpp:1620-1630 */
 __device__ __forceinline__ double step_size(const Params &P, const double x[4], const double k[4]) {
-    /* 1 / (|a / b| + EPS) = b / (|a| + EPS b) with b = |k| + EPS > 0: four divisions instead of
-     * seven (same value to rounding; a = 0 still gives 1 / EPS) */
+    /* 1 / (|a / b| + EPS) = b / d with b = |k| + EPS > 0 and d = |a| + EPS b > 0, so
+     * dl = 1 / (b1/d1 + b2/d2 + b3/d3) = d1 d2 d3 / (b1 d2 d3 + b2 d1 d3 + b3 d1 d2): one division
+     * instead of the reference's seven (same value to a few ulp; d >= 1e-40 b >= 1e-80 and every
+     * product stays far inside the fp64 range) -- it sits on the serial chain of every step */
     const double b1 = fabs(k[1]) + EPS, b2 = fabs(k[2]) + EPS, b3 = fabs(k[3]) + EPS;
-    const double i1 = fdiv(b1, fabs(STEP_EPS * x[1]) + EPS * b1);
-    const double i2 = fdiv(b2, fabs(STEP_EPS * fmin(x[2], P.xe2 - x[2])) + EPS * b2);
-    const double i3 = fdiv(b3, STEP_EPS + EPS * b3);
-    return frcp(i1 + i2 + i3);
+    const double d1 = fabs(STEP_EPS * x[1]) + EPS * b1;
+    const double d2 = fabs(STEP_EPS * fmin(x[2], P.xe2 - x[2])) + EPS * b2;
+    const double d3 = STEP_EPS + EPS * b3;
+    const double d23 = d2 * d3, d12 = d1 * d2;
+    return fdiv(d1 * d23, fma(b1, d23, fma(b2, d1 * d3, b3 * d12)));
 }
 
 /* One attempted push of length dl (body of harm_model.cpp:1230-1277).  Returns the fail

@@ -531,7 +531,10 @@ def zone_shards(zone_weights: np.ndarray, world: int, mode: str = "strided") -> 
     records nothing and one of the escape region records 2-3x the average, which moved the job's
     recorded / scattered counts +17 / +30 / +43 % at 2 / 4 / 8 ranks (tests/test_gpu_multirank.py,
     DESIGN.md §7).  Either way zone streams are keyed by zone, so the union of the shards is exactly
-    the single-GPU photon set."""
+    the single-GPU photon set -- the same initial states.  Transport streams are keyed by photon id,
+    and rank r's ids start after the photons of ranks < r (rank-major), so with strided shards a
+    photon's id, and its transport draws, differ from the single-GPU job's (zone order): the N-rank
+    job is another valid run of the same photons, not a bit-replay."""
     n = len(zone_weights)
     if mode == "strided":
         return [(r, n, world) for r in range(world)]

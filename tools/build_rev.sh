@@ -7,16 +7,21 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 rev=$1; name=$2
 D="$R/cuda-grmonty_amd/build/rev_$name"
 rm -rf "$D"; mkdir -p "$D/csrc" "$D/include"
-for f in grm_engine.hip grm_probe.hip grm_emit.hip grm_tables.hip grm_device.h grm_emit.h; do
+for f in grm_engine.hip grm_lone.hip grm_probe.hip grm_emit.hip grm_tables.hip grm_device.h grm_emit.h; do
   git -C "$R" show "$rev:cuda-grmonty_amd/csrc/$f" > "$D/csrc/$f" 2>/dev/null || rm -f "$D/csrc/$f"
 done
 git -C "$R" show "$rev:include/grmonty_amd.h" > "$D/include/grmonty_amd.h"
-sed -i 's|"../../include/grmonty_amd.h"|"../include/grmonty_amd.h"|' "$D/csrc/"*.h "$D/csrc/"*.hip
+git -C "$R" show "$rev:include/grmonty_amd_debug.h" > "$D/include/grmonty_amd_debug.h" 2>/dev/null || rm -f "$D/include/grmonty_amd_debug.h"
+sed -i 's|"../../include/grmonty_amd|"../include/grmonty_amd|' "$D/csrc/"*.h "$D/csrc/"*.hip
 make -s -C "$R/cuda-grmonty_amd" build/grm_host.o
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -mllvm -disable-machine-licm"
 SF=""; [ -n "$SCHED" ] && SF="-mllvm -amdgpu-sched-strategy=$SCHED"  # revisions before 58fc566 were built with SCHED=iterative-ilp
 /opt/rocm/bin/hipcc $FL $SF $VFLAGS -c "$D/csrc/grm_engine.hip" -o "$D/grm_engine.o" &
 objs="$D/grm_engine.o"
+if [ -f "$D/csrc/grm_lone.hip" ]; then
+  /opt/rocm/bin/hipcc ${FL/-mllvm -disable-machine-licm/} -mllvm -amdgpu-sched-strategy=max-ilp $VFLAGS -c "$D/csrc/grm_lone.hip" -o "$D/grm_lone.o" &
+  objs="$objs $D/grm_lone.o"
+fi
 for f in grm_probe grm_emit grm_tables; do
   [ -f "$D/csrc/$f.hip" ] || continue
   /opt/rocm/bin/hipcc $FL -c "$D/csrc/$f.hip" -o "$D/$f.o" &
