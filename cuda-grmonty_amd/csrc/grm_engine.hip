@@ -2376,6 +2376,7 @@ struct grm_engine {
     int bias_mode = 0;
     uint64_t id_base = 0;
     int grid_override = 0;
+    int64_t flight_ratio = 64; /* GRM_OPT_FLIGHT_RATIO: a live-bias call of n photons runs on <= n / this lanes */
     double max_tau_init = 0.0;
     bool frozen_set = false;
     /* photons; -1 = lanes; -2 (default) = auto: lanes for a call of fewer than WARMUP_AUTO_RATIO x lanes
@@ -2603,9 +2604,10 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
         const uint64_t n_call = pos1 - pos0;
-        const bool small = n_call < WARMUP_AUTO_RATIO * e->lanes;
-        const uint64_t limit = e->warmup == -2 ? (small ? (uint64_t)e->lanes : WARMUP_PHOTONS)
-                               : e->warmup < 0 ? (uint64_t)e->lanes
+        const uint64_t lanes = (uint64_t)grid * BLOCK; /* this call's launch */
+        const bool small = n_call < WARMUP_AUTO_RATIO * lanes;
+        const uint64_t limit = e->warmup == -2 ? (small ? lanes : WARMUP_PHOTONS)
+                               : e->warmup < 0 ? lanes
                                                : (uint64_t)e->warmup;
         C.admit_n = (!e->bias_mode && e->history < limit && pos0 == 0) ? std::min<uint64_t>(pos1, limit - e->history) : 0;
         C.admit_h0 = e->history;
@@ -2680,8 +2682,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         }
         C.ovf = e->d_ovf[dst];
         C.ovf_count = e->d_small + 1 + dst;
-        /* the per-wave record is kept of the first launch on the full grid (the bulk of a call) */
-        C.waves = (pass == 0 && grid == e->grid) ? e->d_waves : nullptr;
+        /* the per-wave record is kept of the first launch (the bulk of a call) */
+        C.waves = pass == 0 ? e->d_waves : nullptr;
         C.phases = C.waves ? e->d_waves + (size_t)(e->lanes / 64) * 4 : nullptr;
         if (C.phases) HIPCHK(e, hipMemsetAsync(C.phases, 0, PHASE_LOG * sizeof(unsigned long long), e->stream));
         if (C.waves) e->waves_rows = (size_t)grid * (BLOCK / 64);
@@ -2813,10 +2815,21 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     if (n == 0) return 0;
     const int sh = n >= (2ull << CLAIM_SH) ? CLAIM_SH : 0;
     const uint64_t m = (n + (1ull << sh) - 1) >> sh, n_pos = m << sh;
-    /* one launch on the full grid: the live-bias warm-up (the first positions in admission batches)
-     * is admission control inside it, and the claims run free as soon as it is over, while the
-     * warm-up's own long-lived photons are still in flight */
-    if (run_passes(e, d_batch, n, sh, m, 0, n_pos, e->grid)) return -1;
+    /* one launch: the live-bias warm-up (the first positions in admission batches) is admission
+     * control inside it, and the claims run free as soon as it is over, while the warm-up's own
+     * long-lived photons are still in flight.  With the live bias the launch has at most
+     * n / flight_ratio lanes (GRM_OPT_FLIGHT_RATIO): the counters bias_func reads trail the claims
+     * by the photons in flight, and a call of 1.45 M photons (photon_n = 1e5) on 131 k lanes moved
+     * recorded / scattered / steps +4.4 / +5.9 / +4.2 % against the serial reference, +1.0 / +1.1 /
+     * +0.9 % on 16 k lanes (96 seeds each, profiles/r04h_grid_sweep96.jsonl) -- for 1.6x the pass
+     * time at that size; a bench pass (14.5 M photons) keeps the full grid */
+    int grid = e->grid;
+    if (!e->bias_mode && e->flight_ratio > 0) {
+        const uint64_t cap_wg = n / ((uint64_t)e->flight_ratio * BLOCK);
+        grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)grid, cap_wg));
+    }
+    e->stats.last_grid = grid;
+    if (run_passes(e, d_batch, n, sh, m, 0, n_pos, grid)) return -1;
     e->id_base += n;
     return 0;
 }
@@ -3004,6 +3017,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
         }
         return 0;
     case GRM_OPT_GRID_BLOCKS: e->grid_override = (int)v; return 0;
+    case GRM_OPT_FLIGHT_RATIO: e->flight_ratio = v < 0 ? 0 : v; return 0;
     case GRM_OPT_ID_BASE: e->id_base = (uint64_t)v; return 0;
     case GRM_OPT_FROZEN_SCATT: e->fz_scatt = (double)v; e->frozen_set = true; return 0;
     case GRM_OPT_FROZEN_REC: e->fz_rec = (double)v; e->frozen_set = true; return 0;
