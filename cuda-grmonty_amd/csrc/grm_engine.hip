@@ -43,7 +43,9 @@ namespace {
  * while the first waits on a gather or a scalar/branch slot (+20% over one wave per SIMD, measured
  * on MI355X).  The per-lane state copies and per-step lane fields take the LDS, so the
  * spectrum goes to a per-workgroup slice in HBM (L2 atomics). */
+#ifndef GRM_BLOCK
 #define GRM_BLOCK 512
+#endif
 constexpr int BLOCK = GRM_BLOCK;
 constexpr int MIN_WAVES_PER_SIMD = BLOCK / 256;
 constexpr int STACK_DEPTH = 16;                 /* scatter-request slots per lane ... */
@@ -79,9 +81,13 @@ struct DevCounters {
     unsigned long long n_tracked, n_children, n_overflow, n_dropped;
     unsigned long long n_primaries, max_nstep, n_long, n_abandoned, abort, n_nan;
     unsigned long long karg_bad; /* track_kernel's kernel-argument check failed (see kargs_check) */
-    unsigned long long pad;
+    /* a multi-rank job's warm-up state of this rank for the others' admission gates (pass blocks
+     * only, see warm_job): photons admitted << 32 + photons in flight (signed), WARM_DONE once the
+     * rank's admission is over */
+    unsigned long long warm;
 };
 static_assert(sizeof(DevCounters) == 16 * 8, "DevCounters layout (grm_engine_debug_counters)");
+constexpr unsigned long long WARM_DONE = 1ull << 63, WARM_HIST = 1ull << 32;
 
 struct LoneRec;
 struct Ctl {
@@ -245,6 +251,30 @@ __device__ __forceinline__ double bias_den(const Params &P, const Ctl &C) {
     const int lo = __builtin_amdgcn_readfirstlane((int)(d & 0xffffffffll));
     const int hi = __builtin_amdgcn_readfirstlane((int)(d >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+/* The job's warm-up state across ranks (n_peers > 1): photons admitted and photons in flight,
+ * summed over the ranks' blocks of this pass (DevCounters::warm; lane r reads rank r's).  A rank
+ * whose admission is over no longer counts its flight (its waves stop reporting ends), a rank that
+ * has not started the pass reads zero.  Converged callers only. */
+__device__ __forceinline__ void warm_job(const Ctl &C, unsigned long long &hist, long long &flight) {
+    const int lane = (int)(threadIdx.x & 63);
+    unsigned long long h = 0;
+    long long f = 0;
+    if (lane < C.n_peers) {
+        const unsigned long long v =
+            __hip_atomic_load(&(C.peers[lane] + C.ctr_slot)->warm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long r = v & ~WARM_DONE;
+        h = (r + (WARM_HIST >> 1)) >> 32; /* flight may be negative between a claim and its undo */
+        f = (v & WARM_DONE) ? 0 : (long long)(r - h * WARM_HIST);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        h += __shfl_xor(h, o);
+        f += __shfl_xor(f, o);
+    }
+    hist = h;
+    flight = f < 0 ? 0 : f;
 }
 
 /* bias_func (harm_model.cpp:1391-1404), same expression and rounding as the reference */
@@ -1851,6 +1881,9 @@ __device__ void record_stuck(const Ctl &C, const Lane &L) {
     }
 }
 
+#ifdef GRM_X_STATE_GLOBAL
+__device__ double g_state[256 * 2 * LDS_DOUBLES_PER_LANE * BLOCK];
+#endif
 __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P_, Ctl C_) {
     KArgsK *const ka = kargs();
     const Ctl &C0 = C_;
@@ -1859,7 +1892,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) < 24) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
 #endif
+#ifdef GRM_X_STATE_GLOBAL
+    /* experiment: the two state copies in HBM ([workgroup][slot][lane], coalesced), freeing their
+     * 88 KB of LDS (a 768-lane workgroup, three waves per SIMD, needs it) */
+    double *lds = g_state + (size_t)blockIdx.x * 2 * LDS_DOUBLES_PER_LANE * BLOCK;
+#else
     __shared__ double lds[2 * LDS_DOUBLES_PER_LANE * BLOCK];
+#endif
     const Slot ph2{lds + threadIdx.x, BLOCK};
     const Slot bk{lds + LDS_DOUBLES_PER_LANE * BLOCK + threadIdx.x, BLOCK};
     const unsigned lane_id = threadIdx.x & 63;
@@ -1933,6 +1972,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 if (stop) { /* abandon: drop the lane photons, the wave's stack and the pool; exit */
                     /* end the admission too, so that waves parked for it wake up and exit */
                     if (lane_id == 0) __hip_atomic_store(C.admit_end, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane_id == 0 && C.n_peers > 1) atomicOr(C.in_flight, WARM_DONE);
                     if (active) {
                         record_stuck(C, L);
                         atomicAdd(&C.ctr->n_abandoned, 1ull);
@@ -1976,9 +2016,18 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                 if (k_pool > 0) {
                     if (warm) {
                         /* warm-up: claim only inside the admitted batch (CAS); once it is claimed and
-                         * nothing is in flight, one wave admits the next batch */
+                         * nothing is in flight, one wave admits the next batch.  In a multi-rank job
+                         * the gate is the job's: every rank's flight against every rank's admitted
+                         * photons (warm_job), so the ranks' batches interleave as one GPU's would
+                         * (each rank gating on its own flight let the job run ahead of its history:
+                         * +5 % recorded at 8 ranks) */
                         long long got = 0;
                         int off = 0;
+                        const bool job = C.n_peers > 1;
+                        unsigned long long j_hist = 0;
+                        long long j_flight = 0;
+                        if (job) warm_job(C, j_hist, j_flight);
+                        const unsigned long long unit = job ? WARM_HIST + 1 : 1; /* admitted + in flight */
                         if (lane_id == 0) {
                             const unsigned long long end =
                                 __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1991,13 +2040,14 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                 if (head < end) {
                                     unsigned long long want = min((unsigned long long)k_pool, end - head);
                                     if (C.admit_spread) want = min(want, C.admit_spread);
-                                    atomicAdd(C.in_flight, want); /* before the claim is visible */
+                                    atomicAdd(C.in_flight, want * unit); /* before the claim is visible */
                                     if (atomicCAS(C.pool_head, head, head + want) == head)
                                         got = (long long)want;
                                     else
-                                        atomicAdd(C.in_flight, (unsigned long long)(-(long long)want));
-                                } else if (__hip_atomic_load(C.in_flight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <=
-                                           ((C.admit_h0 + end) >> C.admit_slack)) {
+                                        atomicAdd(C.in_flight, (unsigned long long)(-(long long)(want * unit)));
+                                } else if (job ? (unsigned long long)j_flight <= (j_hist >> C.admit_slack)
+                                               : __hip_atomic_load(C.in_flight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <=
+                                                     ((C.admit_h0 + end) >> C.admit_slack)) {
                                     /* the next batch once all but a straggler fraction of the history
                                      * has ended: the counters then hold nearly all of it, and one
                                      * long-lived photon does not hold the warm-up up */
@@ -2005,7 +2055,9 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                     const unsigned long long next =
                                         end >= C.admit_n ? ~0ull
                                                          : min(C.admit_n, end + max(C.admit_b0, min(h, C.admit_lim - h)));
-                                    if (atomicCAS(C.admit_end, end, next) == end && C.phases) {
+                                    const bool opened = atomicCAS(C.admit_end, end, next) == end;
+                                    if (opened && next == ~0ull && job) atomicOr(C.in_flight, WARM_DONE);
+                                    if (opened && C.phases) {
                                         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
                                         if (next == ~0ull) C.phases[0] = t;
                                         /* the admission log: [3 + 2k] when batch k + 1 opened, [4 + 2k]
@@ -2104,8 +2156,10 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             if (warm) {
                 /* waiting for the next batch; a barrier that never opens (it cannot, short of a
                  * counting bug) must not hang the GPU: after ~1 s give the warm-up up for all */
-                if (++wait_trips > (1u << 21) && lane_id == 0)
+                if (++wait_trips > (1u << 21) && lane_id == 0) {
                     __hip_atomic_store(C.admit_end, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (C.n_peers > 1) atomicOr(C.in_flight, WARM_DONE);
+                }
                 __builtin_amdgcn_s_sleep(16);
             }
             continue;
@@ -2260,6 +2314,8 @@ struct CtlOp {
     unsigned set;
     int reset, clear_abort;
     unsigned long long max_tau_init_bits;
+    int set_warm;                  /* ctr->warm = warm_val (a multi-rank job's warm-up start) */
+    unsigned long long warm_val;
 };
 
 /* one pass's results into slot `slot` of the stash (grm_engine_stash): the spectrum, then the
@@ -2323,6 +2379,7 @@ __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
         op.ctr->max_tau_bits = op.max_tau_init_bits;
     }
     if (op.clear_abort) op.ctr->abort = 0;
+    if (op.set_warm) op.ctr->warm = op.warm_val;
     for (int i = 0; i < 16; ++i)
         if ((op.set >> i) & 1u) op.small[i] = op.val[i];
     if (op.h_ctr) {
@@ -2376,7 +2433,7 @@ struct grm_engine {
     int bias_mode = 0;
     uint64_t id_base = 0;
     int grid_override = 0;
-    int64_t flight_ratio = 64; /* GRM_OPT_FLIGHT_RATIO: a live-bias call of n photons runs on <= n / this lanes */
+    int64_t flight_ratio = 96; /* GRM_OPT_FLIGHT_RATIO: a live-bias call of n photons runs on <= n / this lanes */
     double max_tau_init = 0.0;
     bool frozen_set = false;
     /* photons; -1 = lanes; -2 (default) = auto: lanes for a call of fewer than WARMUP_AUTO_RATIO x lanes
@@ -2589,7 +2646,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.child_min = e->child_min;
     C.lanes = (int)e->lanes;
     C.bias_frozen = e->bias_mode;
-    C.in_flight = e->d_small + 4;
+    /* a multi-rank job's flight goes to the pass block, where the other ranks' gates read it */
+    C.in_flight = C.n_peers > 1 ? &e->d_ctr->warm : e->d_small + 4;
     C.admit_end = e->d_small + 5;
     C.watchdog_ticks = (unsigned long long)std::max<int64_t>(e->watchdog_ms, 0) * 100000ull; /* 100 MHz */
     C.stuck = e->d_stuck;
@@ -2659,6 +2717,9 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             op.val[4] = 0;
             op.val[5] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
                                                                     C.admit_b0, std::min(h, C.admit_lim - h)));
+            /* the job's gate counts this rank's earlier calls as admitted history */
+            op.set_warm = C.n_peers > 1;
+            op.warm_val = h * WARM_HIST;
         }
         /* the main launch runs the early worker beside it: [8] early tail, [9] head, [10] done,
          * [11] workgroups exited, [12] worker running / closed, [13] bulk started */

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--shared", action="store_true")
     ap.add_argument("--photon-n", type=float, default=1e5)
     ap.add_argument("--seed0", type=int, default=123)
+    ap.add_argument("--opt", action="append", default=[], help="engine option K=V (grmonty_amd.OPT_*), experiments")
     args = ap.parse_args()
     import numpy as np
     import grmonty_amd as G
@@ -38,6 +39,9 @@ def main():
     for r in range(world):
         e = G.Engine(model, device=0)
         e.set_option(G.OPT_GRID_BLOCKS, max(1, 256 // world))
+        for kv in args.opt:
+            k, v = kv.split("=")
+            e.set_option(int(k), int(v))
         e.emit_setup(model)
         e.stash_reserve(args.seeds)
         engines.append(e)
