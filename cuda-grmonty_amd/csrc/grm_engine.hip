@@ -162,7 +162,10 @@ struct Ctl {
     int n_peers, ctr_slot;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
-constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
+#ifndef GRM_REFRESH_TRIPS
+#define GRM_REFRESH_TRIPS 64
+#endif
+constexpr unsigned REFRESH_TRIPS = GRM_REFRESH_TRIPS; /* counter flush + bias refresh + watchdog period (power of 2) */
 
 /* Per-step (or rarer) lane fields: an LDS column per lane ([field][lane], conflict-free), read and
  * written where used -- what brings the kernel's register demand under the 256 VGPRs two waves per
@@ -2051,10 +2054,21 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                     /* the next batch once all but a straggler fraction of the history
                                      * has ended: the counters then hold nearly all of it, and one
                                      * long-lived photon does not hold the warm-up up */
-                                    const unsigned long long h = C.admit_h0 + end;
+                                    /* one GPU: the batch doubles the history, up to admit_lim.  A job
+                                     * (n_peers ranks): this rank's share of a batch that doubles the JOB's
+                                     * admitted photons, and the admission ends for every rank when the job's
+                                     * reach admit_lim (= n_peers x one GPU's); sized from its own history, a
+                                     * rank that won a few gate openings ran its batches ahead of the others
+                                     * and left the warm-up early, on a history far shorter than the job's
+                                     * in flight (+4-5 % recorded at 2-8 emulated ranks, round 4) */
+                                    const unsigned long long h = job ? j_hist : C.admit_h0 + end;
+                                    const unsigned long long grow =
+                                        job ? min(h, C.admit_lim - min(h, C.admit_lim)) / (unsigned long long)C.n_peers
+                                            : min(h, C.admit_lim - h);
                                     const unsigned long long next =
-                                        end >= C.admit_n ? ~0ull
-                                                         : min(C.admit_n, end + max(C.admit_b0, min(h, C.admit_lim - h)));
+                                        (end >= C.admit_n || (job && h >= C.admit_lim))
+                                            ? ~0ull
+                                            : min(C.admit_n, end + max(C.admit_b0, grow));
                                     const bool opened = atomicCAS(C.admit_end, end, next) == end;
                                     if (opened && next == ~0ull && job) atomicOr(C.in_flight, WARM_DONE);
                                     if (opened && C.phases) {
@@ -2414,6 +2428,7 @@ struct grm_engine {
     DevCounters *d_ctr_slots = nullptr; /* per-pass blocks (grm_engine_stash_reserve), shared with peers */
     int n_ctr_slots = 0, ctr_slot = -1;
     const DevCounters **d_peers = nullptr; /* device array: every rank's d_ctr_slots */
+    const DevCounters *peer0 = nullptr;    /* rank 0's d_ctr_slots (experiment GRM_X_SHARED_BLOCK) */
     int n_peers = 0;
     std::vector<void *> ipc_open;           /* peers' blocks opened by IPC (closed at destroy) */
     grm_spectrum_cell *d_spec = nullptr;
@@ -2638,6 +2653,13 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.peers = e->d_peers;
     C.n_peers = (e->ctr_slot >= 0 && e->d_peers) ? e->n_peers : 0;
     C.ctr_slot = e->ctr_slot;
+#ifdef GRM_X_SHARED_BLOCK
+    /* experiment: every rank counts into rank 0's block of the pass and reads it as one GPU does */
+    if (C.n_peers > 1) {
+        C.ctr = const_cast<DevCounters *>(e->peer0) + e->ctr_slot;
+        C.n_peers = 0;
+    }
+#endif
     C.trace = e->trace_cap ? e->d_trace : nullptr;
     C.trace_cap = e->trace_cap;
     C.trace_count = e->d_small + 3;
@@ -2667,9 +2689,11 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         const uint64_t limit = e->warmup == -2 ? (small ? lanes : WARMUP_PHOTONS)
                                : e->warmup < 0 ? lanes
                                                : (uint64_t)e->warmup;
-        C.admit_n = (!e->bias_mode && e->history < limit && pos0 == 0) ? std::min<uint64_t>(pos1, limit - e->history) : 0;
+        /* a multi-rank job ramps the job's history to n_peers x one GPU's warm-up (see the kernel) */
+        const uint64_t lim = C.n_peers > 1 ? limit * (uint64_t)C.n_peers : limit;
+        C.admit_n = (!e->bias_mode && e->history < lim && pos0 == 0) ? std::min<uint64_t>(pos1, lim - e->history) : 0;
         C.admit_h0 = e->history;
-        C.admit_lim = limit;
+        C.admit_lim = lim;
         C.admit_slack = e->warmup_slack >= 0 ? e->warmup_slack : (e->warmup == -2 && small ? 4 : WARMUP_SLACK_LARGE);
         /* With the job's counters (n_peers ranks), every rank ramps at once: its batches are 1/n_peers
          * of a single GPU's, so that the JOB admits 64, 64, 128, ... photons against the job-wide
@@ -2715,8 +2739,9 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             const unsigned long long h = C.admit_h0;
             op.set |= (1u << 4) | (1u << 5);
             op.val[4] = 0;
+            const unsigned long long n_r = C.n_peers > 1 ? (unsigned long long)C.n_peers : 1ull;
             op.val[5] = std::min<unsigned long long>(C.admit_n, std::max<unsigned long long>(
-                                                                    C.admit_b0, std::min(h, C.admit_lim - h)));
+                                                                    C.admit_b0, std::min(h, C.admit_lim - h) / n_r));
             /* the job's gate counts this rank's earlier calls as admitted history */
             op.set_warm = C.n_peers > 1;
             op.warm_val = h * WARM_HIST;
@@ -3463,6 +3488,7 @@ int upload_peers(grm_engine *e, const std::vector<const DevCounters *> &tab) {
     e->d_peers = nullptr;
     e->n_peers = 0;
     if (tab.size() < 2) return 0;
+    e->peer0 = tab[0];
     HIPCHK(e, hipMalloc(&e->d_peers, tab.size() * sizeof(DevCounters *)));
     HIPCHK(e, hipMemcpy(e->d_peers, tab.data(), tab.size() * sizeof(DevCounters *), hipMemcpyHostToDevice));
     e->n_peers = (int)tab.size();

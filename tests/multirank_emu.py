@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--shared", action="store_true")
     ap.add_argument("--photon-n", type=float, default=1e5)
     ap.add_argument("--seed0", type=int, default=123)
+    ap.add_argument("--sequential", action="store_true", help="ranks one after another (experiments)")
     ap.add_argument("--opt", action="append", default=[], help="engine option K=V (grmonty_amd.OPT_*), experiments")
     args = ap.parse_args()
     import numpy as np
@@ -69,16 +70,22 @@ def main():
                 if stt["n_dropped"] or stt["n_abandoned"]:
                     raise RuntimeError("photons lost")
                 spec, nr, ns, mt = e.finish()
-                out[r] = dict(spec=spec, created=n, recorded=nr, scattered=ns, steps=stt["n_steps"], max_tau=mt)
+                out[r] = dict(spec=spec, created=n, recorded=nr, scattered=ns, steps=stt["n_steps"], max_tau=mt,
+                              rec_spec=float(spec["nph"].sum()), scatt_spec=float(spec["nscatt"].sum()))
             except Exception as ex:  # reported below
                 err.append(repr(ex))
                 go.abort()
 
-        th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
+        if args.sequential:  # each rank's pass alone, in rank order (no barrier)
+            go = threading.Barrier(1)
+            for r in range(world):
+                rank(r)
+        else:
+            th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
         if err:
             raise RuntimeError(err[0])
         spec = out[0]["spec"].copy()
@@ -92,6 +99,9 @@ def main():
         job["max_tau"] = max(o["max_tau"] for o in out)
         job["job_view"] = [e.job_counters() for e in engines] if args.shared else None
         job["per_rank_recorded"] = [o["recorded"] for o in out]
+        # the spectrum's own sums (independent of the counter blocks)
+        job["rec_spec"] = sum(o["rec_spec"] for o in out)
+        job["scatt_spec"] = sum(o["scatt_spec"] for o in out)
         res.append(job)
         print(json.dumps({k: v for k, v in job.items() if k != "job_view"}), flush=True)
     for e in engines:

@@ -27,10 +27,12 @@ def main():
         f = spec.split(":")
         name, world, seeds = f[0], int(f[1]), int(f[2])
         shared = "shared" in f[3:]
-        opts = [kv for x in f[3:] if x != "shared" for kv in x.split(",") if kv]
+        seq = "seq" in f[3:]
+        opts = [kv for x in f[3:] if x not in ("shared", "seq") for kv in x.split(",") if kv]
         tmp = os.path.join(R, "gpurun_out", f"emu_{name}.json")
         cmd = [sys.executable, "-u", os.path.join(R, "tests", "multirank_emu.py"), dump, str(world), str(seeds), tmp]
         cmd += ["--shared"] if shared else []
+        cmd += ["--sequential"] if seq else []
         for kv in opts:
             cmd += ["--opt", kv]
         env = dict(os.environ, GPU_MAX_HW_QUEUES=str(min(32, 2 * world + 2)))
@@ -41,7 +43,10 @@ def main():
         jobs = json.load(open(tmp))
         row = {"name": name, "world": world, "seeds": seeds, "shared": shared, "opts": opts}
         for k in KEYS:
-            dev = [j[k] for j in jobs]
+            # with the counters in rank 0's block (variant library "sb") the per-rank counter reads
+            # are incomplete: recorded / scattered from the spectra's own sums
+            src = {"recorded": "rec_spec", "scattered": "scatt_spec"}.get(k, k) if "sb" in name else k
+            dev = [j[src] for j in jobs]
             diff, se, z = welch_z(dev, o[k])
             row[k] = {"mean": float(np.mean(dev)), "diff": float(diff / o[k].mean()), "z": float(z)}
         print(f"{name:14s} world {world} {'shared' if shared else 'own'} {opts}: " +
