@@ -43,9 +43,7 @@ namespace {
  * while the first waits on a gather or a scalar/branch slot (+20% over one wave per SIMD, measured
  * on MI355X).  The per-lane state copies and per-step lane fields take the LDS, so the
  * spectrum goes to a per-workgroup slice in HBM (L2 atomics). */
-#ifndef GRM_BLOCK
 #define GRM_BLOCK 512
-#endif
 constexpr int BLOCK = GRM_BLOCK;
 constexpr int MIN_WAVES_PER_SIMD = BLOCK / 256;
 constexpr int STACK_DEPTH = 16;                 /* scatter-request slots per lane ... */
@@ -162,10 +160,7 @@ struct Ctl {
     int n_peers, ctr_slot;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
-#ifndef GRM_REFRESH_TRIPS
-#define GRM_REFRESH_TRIPS 64
-#endif
-constexpr unsigned REFRESH_TRIPS = GRM_REFRESH_TRIPS; /* counter flush + bias refresh + watchdog period (power of 2) */
+constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
 
 /* Per-step (or rarer) lane fields: an LDS column per lane ([field][lane], conflict-free), read and
  * written where used -- what brings the kernel's register demand under the 256 VGPRs two waves per
@@ -1884,9 +1879,6 @@ __device__ void record_stuck(const Ctl &C, const Lane &L) {
     }
 }
 
-#ifdef GRM_X_STATE_GLOBAL
-__device__ double g_state[256 * 2 * LDS_DOUBLES_PER_LANE * BLOCK];
-#endif
 __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params P_, Ctl C_) {
     KArgsK *const ka = kargs();
     const Ctl &C0 = C_;
@@ -1895,13 +1887,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) < 24) g_tlds[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x & 63) == 15 ? t_start : 0;
 #endif
-#ifdef GRM_X_STATE_GLOBAL
-    /* experiment: the two state copies in HBM ([workgroup][slot][lane], coalesced), freeing their
-     * 88 KB of LDS (a 768-lane workgroup, three waves per SIMD, needs it) */
-    double *lds = g_state + (size_t)blockIdx.x * 2 * LDS_DOUBLES_PER_LANE * BLOCK;
-#else
     __shared__ double lds[2 * LDS_DOUBLES_PER_LANE * BLOCK];
-#endif
     const Slot ph2{lds + threadIdx.x, BLOCK};
     const Slot bk{lds + LDS_DOUBLES_PER_LANE * BLOCK + threadIdx.x, BLOCK};
     const unsigned lane_id = threadIdx.x & 63;
@@ -2428,7 +2414,6 @@ struct grm_engine {
     DevCounters *d_ctr_slots = nullptr; /* per-pass blocks (grm_engine_stash_reserve), shared with peers */
     int n_ctr_slots = 0, ctr_slot = -1;
     const DevCounters **d_peers = nullptr; /* device array: every rank's d_ctr_slots */
-    const DevCounters *peer0 = nullptr;    /* rank 0's d_ctr_slots (experiment GRM_X_SHARED_BLOCK) */
     int n_peers = 0;
     std::vector<void *> ipc_open;           /* peers' blocks opened by IPC (closed at destroy) */
     grm_spectrum_cell *d_spec = nullptr;
@@ -2653,13 +2638,6 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.peers = e->d_peers;
     C.n_peers = (e->ctr_slot >= 0 && e->d_peers) ? e->n_peers : 0;
     C.ctr_slot = e->ctr_slot;
-#ifdef GRM_X_SHARED_BLOCK
-    /* experiment: every rank counts into rank 0's block of the pass and reads it as one GPU does */
-    if (C.n_peers > 1) {
-        C.ctr = const_cast<DevCounters *>(e->peer0) + e->ctr_slot;
-        C.n_peers = 0;
-    }
-#endif
     C.trace = e->trace_cap ? e->d_trace : nullptr;
     C.trace_cap = e->trace_cap;
     C.trace_count = e->d_small + 3;
@@ -3488,7 +3466,6 @@ int upload_peers(grm_engine *e, const std::vector<const DevCounters *> &tab) {
     e->d_peers = nullptr;
     e->n_peers = 0;
     if (tab.size() < 2) return 0;
-    e->peer0 = tab[0];
     HIPCHK(e, hipMalloc(&e->d_peers, tab.size() * sizeof(DevCounters *)));
     HIPCHK(e, hipMemcpy(e->d_peers, tab.data(), tab.size() * sizeof(DevCounters *), hipMemcpyHostToDevice));
     e->n_peers = (int)tab.size();
