@@ -421,8 +421,8 @@ class Engine:
         adm = (C.c_uint64 * 64)()
         k = self.L.grm_engine_debug_admissions(self.h, adm, 32)
         batches = [(ms(adm[2 * i]), int(adm[2 * i + 1])) for i in range(max(0, min(k, 32)))]
-        return {"warmup_end_ms": ms(out[1]), "pool_drained_ms": ms(out[2]), "last_exit_ms": ms(out[3]),
-                "admissions": batches}
+        return {"t0_ticks": int(t0), "warmup_end_ms": ms(out[1]), "pool_drained_ms": ms(out[2]),
+                "last_exit_ms": ms(out[3]), "admissions": batches}
 
     def debug_counters(self) -> dict:
         """raw device counters (grm_engine_debug_counters)"""

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--photon-n", type=float, default=1e5)
     ap.add_argument("--seed0", type=int, default=123)
     ap.add_argument("--sequential", action="store_true", help="ranks one after another (experiments)")
+    ap.add_argument("--phases", action="store_true", help="per-rank launch phases (diagnostics)")
     ap.add_argument("--opt", action="append", default=[], help="engine option K=V (grmonty_amd.OPT_*), experiments")
     args = ap.parse_args()
     import numpy as np
@@ -71,7 +72,8 @@ def main():
                     raise RuntimeError("photons lost")
                 spec, nr, ns, mt = e.finish()
                 out[r] = dict(spec=spec, created=n, recorded=nr, scattered=ns, steps=stt["n_steps"], max_tau=mt,
-                              rec_spec=float(spec["nph"].sum()), scatt_spec=float(spec["nscatt"].sum()))
+                              rec_spec=float(spec["nph"].sum()), scatt_spec=float(spec["nscatt"].sum()),
+                              phases=e.debug_phases() if args.phases else None)
             except Exception as ex:  # reported below
                 err.append(repr(ex))
                 go.abort()
@@ -99,6 +101,10 @@ def main():
         job["max_tau"] = max(o["max_tau"] for o in out)
         job["job_view"] = [e.job_counters() for e in engines] if args.shared else None
         job["per_rank_recorded"] = [o["recorded"] for o in out]
+        job["per_rank_created"] = [o["created"] for o in out]
+        job["per_rank_scattered"] = [o["scattered"] for o in out]
+        if args.phases:
+            job["per_rank_phases"] = [o["phases"] for o in out]
         # the spectrum's own sums (independent of the counter blocks)
         job["rec_spec"] = sum(o["rec_spec"] for o in out)
         job["scatt_spec"] = sum(o["scatt_spec"] for o in out)
