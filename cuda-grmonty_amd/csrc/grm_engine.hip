@@ -2672,7 +2672,12 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.admit_n = (!e->bias_mode && e->history < lim && pos0 == 0) ? std::min<uint64_t>(pos1, lim - e->history) : 0;
         C.admit_h0 = e->history;
         C.admit_lim = lim;
-        C.admit_slack = e->warmup_slack >= 0 ? e->warmup_slack : (e->warmup == -2 && small ? 4 : WARMUP_SLACK_LARGE);
+        /* slack: 1/16 for the small-call ramp and for a multi-rank job (its ranks' batches interleave
+         * in 1/N shares; emulated 8-rank jobs, 48 each against the oracle at photon_n = 1e5: +4.1 to
+         * +5.5 % recorded at 1/2 over five sessions, +2.3 / +2.4 / +3.1 % at 1/16 with warm-ups of 4 k /
+         * 16 k / 64 k photons per rank, profiles/r04r_emu_sweep.log, r04y_emu.log) */
+        C.admit_slack = e->warmup_slack >= 0 ? e->warmup_slack
+                                              : ((e->warmup == -2 && small) || C.n_peers > 1 ? 4 : WARMUP_SLACK_LARGE);
         /* With the job's counters (n_peers ranks), every rank ramps at once: its batches are 1/n_peers
          * of a single GPU's, so that the JOB admits 64, 64, 128, ... photons against the job-wide
          * history as one GPU does (each rank at full batches would start n_peers x 64 photons on the
