@@ -202,11 +202,17 @@ int grm_emit_launch(const Params &P, const EmitParams &E, uint64_t z0, uint64_t 
     if (!chk(hipGetLastError(), "zone_count_scan") || !chk(hipStreamSynchronize(s), "sync")) return -1;
     const unsigned long long total = *(volatile unsigned long long *)h_total;
     if (total > *out_cap) {
+        /* grown with 1/8 headroom: the count moves by ~0.1 % from seed to seed, and an exact fit
+         * reallocated whenever a pass drew more photons than every pass before -- hipFree waits
+         * for the whole device, so one engine's emission then waited for every other stream's
+         * work (the emulated ranks sharing a GPU started up to 0.5 s late, profiles/r04v_phases_w8.log),
+         * and a bench pass paid the free + malloc of ~2 GB in its timed region */
         if (*out) (void)hipFree(*out);
         *out = nullptr;
         *out_cap = 0;
-        if (!chk(hipMalloc(out, total * sizeof(grm_init_photon)), "emit buffer")) return -1;
-        *out_cap = total;
+        const unsigned long long cap = total + total / 8;
+        if (!chk(hipMalloc(out, cap * sizeof(grm_init_photon)), "emit buffer")) return -1;
+        *out_cap = cap;
     }
     if (total > 0) {
         const uint64_t blocks = (total + EMIT_BLOCK - 1) / EMIT_BLOCK;

@@ -3109,11 +3109,11 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
 int grm_engine_track(grm_engine *e, const grm_init_photon *batch, size_t n) {
     if (!e || (!batch && n)) return -1;
     HIPCHK(e, hipSetDevice(e->device));
-    if (n > e->batch_cap) {
+    if (n > e->batch_cap) { /* 1/8 headroom, as the emission buffer (grm_emit.hip) */
         if (e->d_batch) hipFree(e->d_batch);
         e->d_batch = nullptr;
-        HIPCHK(e, hipMalloc(&e->d_batch, n * sizeof(grm_init_photon)));
-        e->batch_cap = n;
+        HIPCHK(e, hipMalloc(&e->d_batch, (n + n / 8) * sizeof(grm_init_photon)));
+        e->batch_cap = n + n / 8;
     }
     HIPCHK(e, hipMemcpyAsync(e->d_batch, batch, n * sizeof(grm_init_photon), hipMemcpyHostToDevice, e->stream));
     return run_transport(e, e->d_batch, n);
