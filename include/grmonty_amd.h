@@ -158,7 +158,8 @@ enum {
     GRM_OPT_CHILD_MIN = 11,
     /* warm-up straggler tolerance, log2: the next admission batch starts once at most 1/2^slack of
      * the history is still in flight (default -1 = auto: 4 for the small-pass ramp to a grid of
-     * lanes, 1 for the 4,096-photon warm-up of larger passes) */
+     * lanes and for a multi-rank job's warm-up (grm_engine_set_peers / grm_engine_link_peers), 1 for
+     * the 4,096-photon warm-up of a single GPU's larger passes) */
     GRM_OPT_WARMUP_SLACK = 12,
     /* 1 (default): a wave whose only work left is one photon hands it to the lone-photon kernel (two
      * waves per photon, after the launch); 0: the lane loop keeps it; 2: every photon is handed over
