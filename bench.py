@@ -448,6 +448,13 @@ def main():
                        "dominant_launch_ms_per_pass": big_ms / args.steps,
                        "emit_ms_per_pass": emit_ms / args.steps,
                        "longest_photon_life_steps": max(s["max_photon_steps"] for s in sts),
+                       # where each pass's time went beyond its bulk launch: the early worker's launch (beside
+                       # the bulk), the lone-photon kernels after it, the photons they took, the longest life
+                       "tail_per_pass": [{"bulk_ms": round(s["max_launch_ms"], 1), "early_ms": round(s["early_ms"], 1),
+                                          "n_early": s["n_early"], "lone_ms": round(s["lone_ms"], 1),
+                                          "n_lone": s["n_lone"], "kernels_ms": round(s["last_kernel_ms"], 1),
+                                          "longest_life": s["max_photon_steps"], "lives_gt_1e5": s["n_long_photons"]}
+                                         for s in sts],
                        "tracked_per_pass": sum(s["n_tracked"] for s in sts) // args.steps,
                        "children_per_pass": sum(s["n_children"] for s in sts) // args.steps,
                        "recorded_per_pass": sum(r[2] for r in res) // args.steps,
