@@ -10,7 +10,8 @@
    unbiased whatever the bias) and the counters the live bias drives (recorded, scattered, steps)
    within Z_MAX combined standard errors (no allowance: the sharding faults this test exists for
    are +17 to +43 %, below, and the job's warm-up now ramps job-wide -- each rank admits 1/N of a
-   single GPU's batches, grm_engine.hip run_passes); and every rank's view of the job counters (the
+   single GPU's batches behind a barrier at 1/16 of the job's history, grm_engine.hip run_passes,
+   DESIGN.md §7: 8 ranks +5 % at 1/2, +1.2 to +3.7 % at 1/16); and every rank's view of the job counters (the
    kernels' own summation path) must equal the sums of the ranks'.
    Without the link each rank's bias runs on its own history, N times shorter: +18 / +30 / +35 %
    recorded at 2 / 4 / 8 ranks with strided shards (profiles/r03b_pytest_multirank_unshared.log),
