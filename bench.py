@@ -148,13 +148,15 @@ PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def committed_traffic():
-    """HBM bytes per dominant track_kernel launch measured by rocprofv3 PMC passes over this same
-    bench command (tools/traffic_summary.py -> profiles/pmc_traffic.json), or None"""
+    """(HBM bytes per dominant track_kernel launch, the PMC file's provenance) measured by rocprofv3
+    PMC passes over this same bench command (tools/traffic_summary.py -> profiles/pmc_traffic.json,
+    regenerated on the tree it describes), or (None, None)"""
     try:
         with open(PMC_TRAFFIC) as fh:
-            return json.load(fh)["bytes_per_dominant_launch"]
+            d = json.load(fh)
+        return d["bytes_per_dominant_launch"], d.get("source", PMC_TRAFFIC.replace(REPO + "/", ""))
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 def pmc_traffic(path: str):
@@ -251,6 +253,12 @@ def main():
     engine.emit_setup(model)  # the zone table is resident in HBM before the timed region
     bias_counters = "single GPU"
     valid_for_parity = True
+    if args.shard_of and part_world > 1:
+        # one rank's shard alone: its adaptive bias runs on its own history, 1/N of the job's (DESIGN.md
+        # §7: +35 % recorded at 8 ranks with per-rank counters), so its work per photon -- and this
+        # line's rate -- are not the reference's counters
+        bias_counters = "per shard (this rank's own history, 1/N of the job's)"
+        valid_for_parity = False
     # pre-flight: which of the job's GPUs this rank can read over xGMI (hipDeviceCanAccessPeer)
     peer_row = [int(d == local or G.lib().grm_device_peer_ok(local, d) == 1) for d in sorted(set(devs))]
     peer_matrix = [peer_row]
@@ -389,7 +397,10 @@ def main():
         emit_ms = sum(s["last_emit_ms"] for s in sts)
         cnt = fp64_count()
         flops_step = cnt["flops_per_step"] if cnt else None
-        traffic = pmc_traffic(args.pmc_summary) if args.pmc_summary else committed_traffic()
+        traffic, traffic_src = ((pmc_traffic(args.pmc_summary), "--pmc-summary CSVs of this run") if args.pmc_summary
+                                else committed_traffic())
+        # measured HBM rate of the dominant launch: PMC bytes per launch / this run's launch time
+        hbm_gbs = traffic / (big_ms / args.steps * 1e-3) / 1e9 if traffic else None
         achieved_tf = big_steps * flops_step / (big_ms * 1e-3) / 1e12 if flops_step else None
         alg_gbs = big_steps * ALG_BYTES_PER_STEP / (big_ms * 1e-3) / 1e9
         cpu = None
@@ -433,17 +444,22 @@ def main():
                          "traffic": traffic,
                          "flops_per_step": flops_step,
                          "transcendentals_per_step": cnt.get("transcendentals_per_step") if cnt else None,
+                         "traffic_source": traffic_src,
+                         "hbm_gbs": hbm_gbs, "hbm_measured_frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs else None,
                          "hbm_algorithmic_gbs": alg_gbs, "hbm_frac": alg_gbs / HBM_PEAK_GBS,
                          "note": f"dominant track_kernel launch per pass (alone on the GPU): "
                                  f"{big_steps // args.steps} transport steps in {big_ms / args.steps:.1f} ms "
                                  f"(HIP events on the engine stream) x {flops_step} counted FP64 flops/step "
                                  f"({FP64_COUNT.replace(REPO + '/', '')}); HBM view: {ALG_BYTES_PER_STEP} algorithmic "
-                                 f"B/step -> {alg_gbs:.0f} GB/s; traffic = PMC FETCH(x2)+WRITE bytes per dominant "
+                                 f"B/step -> {alg_gbs:.0f} GB/s (mostly L2 hits); traffic = PMC FETCH(x2)+WRITE bytes per dominant "
                                  f"launch (--pmc-summary CSVs of this run, else profiles/pmc_traffic.json: the PMC passes of this bench "
-                                 f"command, tools/traffic_summary.py)"},
+                                 f"command, tools/traffic_summary.py); hbm_gbs = traffic / this run's dominant launch time"},
             "cpu_baseline": cpu,
             "detail": {"pass_s": {"min": srt[0], "median": srt[len(srt) // 2], "max": srt[-1],
                                   "all": [round(v, 4) for v in pass_s]},
+                       # the rate of the median pass (value is the whole job's: the long-photon tail passes
+                       # weigh in there)
+                       "median_pass_rate": (total / args.steps) / srt[len(srt) // 2],
                        "transport_steps_per_s": steps_tot / (kern_ms * 1e-3), "kernel_ms_per_pass": kern_ms / args.steps,
                        "dominant_launch_ms_per_pass": big_ms / args.steps,
                        "emit_ms_per_pass": emit_ms / args.steps,

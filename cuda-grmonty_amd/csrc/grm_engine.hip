@@ -2065,8 +2065,12 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                         const unsigned long long k = atomicAdd(C.phases + 2, 1ull);
                                         if (k < (PHASE_LOG - 3) / 2) {
                                             C.phases[3 + 2 * k] = t;
-                                            C.phases[4 + 2 * k] = __hip_atomic_load(C.in_flight, __ATOMIC_RELAXED,
-                                                                                    __HIP_MEMORY_SCOPE_AGENT);
+                                            /* photons in flight: a multi-rank pass block packs them into
+                                             * the signed low word of its warm-up state (see DevCounters) */
+                                            const unsigned long long f =
+                                                __hip_atomic_load(C.in_flight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                            const long long fl = job ? (long long)(int)(unsigned)f : (long long)f;
+                                            C.phases[4 + 2 * k] = (unsigned long long)(fl < 0 ? 0 : fl);
                                         }
                                     }
                                 }
@@ -2610,8 +2614,11 @@ constexpr unsigned long long WARMUP_SPREAD = 4;
 int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, uint64_t m, uint64_t pos0,
                uint64_t pos1, int grid) {
     if (pos1 <= pos0) return 0;
-    /* overflow pool: children rarely spill (8-deep lane stacks); size ~ max(1M, n/4) */
-    if (ensure_ovf(e, std::max<unsigned long long>(1ull << 20, (pos1 - pos0) / 4))) return -1;
+    /* overflow pool: children rarely spill (a 1,024-deep stack per wave): a few hundred per
+     * photon_n = 1e6 pass, 213-238 for the 1.8e8-photon shard of BASELINE configs[3]; size
+     * max(1M, n/32) -- 2 x 1.1 GB for that shard, so eight such engines fit one GPU (n/4 took
+     * 2 x 8.8 GB each).  A child that fits nowhere is counted and fails the call (n_dropped). */
+    if (ensure_ovf(e, std::max<unsigned long long>(1ull << 20, (pos1 - pos0) / 32))) return -1;
     if (e->lone == 2 && e->lone_cap < e->ovf_cap + n) { /* test mode: every photon may be handed over */
         if (e->d_lone) (void)hipFree(e->d_lone);
         e->d_lone = nullptr;
@@ -2891,10 +2898,13 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
      * by the photons in flight, and a call of 1.45 M photons (photon_n = 1e5) on 131 k lanes moved
      * recorded / scattered / steps +4.4 / +5.9 / +4.2 % against the serial reference, +1.0 / +1.1 /
      * +0.9 % on 16 k lanes (96 seeds each, profiles/r04h_grid_sweep96.jsonl) -- for 1.6x the pass
-     * time at that size; a bench pass (14.5 M photons) keeps the full grid */
+     * time at that size; a bench pass (14.5 M photons) keeps the full grid.  The lag matters against
+     * the history the counters already hold, so the cap counts the photons tracked since the reset
+     * too: a pass fed in chunks (INTEGRATION.md path (a), 4 M photons per call) runs its later
+     * chunks on the full grid */
     int grid = e->grid;
     if (!e->bias_mode && e->flight_ratio > 0) {
-        const uint64_t cap_wg = n / ((uint64_t)e->flight_ratio * BLOCK);
+        const uint64_t cap_wg = (e->history + n) / ((uint64_t)e->flight_ratio * BLOCK);
         grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)grid, cap_wg));
     }
     e->stats.last_grid = grid;
@@ -3102,6 +3112,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
+    case 18: case 20: case 21: e->err = "retired option " + std::to_string(opt); return -1;
     default: e->err = "unknown option"; return -1;
     }
 }

@@ -55,7 +55,7 @@ OPT_EARLY_STEPS = 15
 OPT_EARLY_SERIAL = 16
 OPT_KARG_TEST = 17
 OPT_WARMUP_SPREAD = 19
-OPT_FLIGHT_RATIO = 20
+OPT_FLIGHT_RATIO = 22
 N_TH_BINS, N_E_BINS = 6, 200
 
 

@@ -182,14 +182,16 @@ enum {
      * batch, and its photons' scattering families, over more waves (0: as many lanes as it has idle;
      * -1, the default: 4 in the 4,096-photon warm-up, 0 in the ramp of a small pass) */
     GRM_OPT_WARMUP_SPREAD = 19,
-    /* live bias: a transport call of n photons runs on at most n / this many lanes (whole
-     * workgroups, at least one; default 96; 0 = always the full grid).  bias_func's counters
-     * (harm_model.cpp:1391-1404) trail the claims by the photons in flight; measured at 192^2,
-     * photon_n = 1e5 (1.45 M photons, 96 seeds each): recorded +4.4 % against the
-     * reference with 131 k lanes in flight, +2.3 % with 22.5 k (ratio 64), +1.0 % with 16 k.  A bench pass (photon_n = 1e6, 14.5 M
-     * photons) keeps the full grid; a frozen bias (GRM_OPT_BIAS_MODE = 1) always does.  (Option 20
-     * and 21 were GRM_OPT_WARMUP_BLOCKS / _WAVES, retired in round 4.) */
-    GRM_OPT_FLIGHT_RATIO = 20
+    /* 20, 21: retired (GRM_OPT_WARMUP_BLOCKS / _WAVES, round 4); setting them is an error */
+    /* live bias: a transport call runs on at most (h + n) / this many lanes, n = the call's photons,
+     * h = the photons tracked since the last reset (whole workgroups, at least one; default 96;
+     * 0 = always the full grid).  bias_func's counters (harm_model.cpp:1391-1404) trail the claims by
+     * the photons in flight, which matters only while the history behind them is short; measured at
+     * 192^2, photon_n = 1e5 (1.45 M photons in one call, 96 seeds each): recorded +4.4 %
+     * against the reference with 131 k lanes in flight, +2.3 % with 22.5 k (ratio 64), +1.0 % with
+     * 16 k.  A bench pass (photon_n = 1e6, 14.5 M photons) keeps the full grid, and so do the later
+     * batches of a pass fed in chunks; a frozen bias (GRM_OPT_BIAS_MODE = 1) always does. */
+    GRM_OPT_FLIGHT_RATIO = 22
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

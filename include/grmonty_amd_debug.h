@@ -31,7 +31,9 @@ int64_t grm_engine_debug_waves(grm_engine *e, uint64_t *out, size_t cap);
 int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap);
 /* raw device counters: n_recorded, n_scatt, max_tau_scatt bits, n_steps, n_tracked, n_children,
  * n_overflow, n_dropped, n_primaries, max photon steps, lives > 1e5 steps, n_abandoned, abort, n_nan,
- * waves whose kernel-argument check failed, 1 reserved */
+ * waves whose kernel-argument check failed, and word 15 = the multi-rank warm-up state of the
+ * pass block (photons admitted << 32, plus the photons in flight as a signed low word, plus bit 63
+ * once this rank's admission is over; 0 on a single GPU) */
 int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]);
 /* diagnostic: the phases of the last call's main launch, s_memrealtime ticks (100 MHz): first wave
  * start, end of the live-bias warm-up admission (0 = none), the pool's last claim chunk taken (0 =

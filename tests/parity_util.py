@@ -10,7 +10,9 @@ harm_model.cpp:1291-1335), which must agree to SPEC_RTOL everywhere else.
 """
 import numpy as np
 
-MIN_MATCH = 0.99       # observed: 1.0000 (r01/r02 GPU logs); a flip is a last-bit event
+MIN_MATCH = 0.998      # observed: 1.0000 in every driver run (r01-r04); a flip is a last-bit event
+# weight / energy of matching photons: the largest relative differences observed over the four
+# transport variants and 512^2 are printed by every test (match_residuals); the bars are ~10x those
 W_RTOL, E_RTOL = 1e-6, 1e-9
 SPEC_RTOL = 1e-6       # per-cell sums of matching photons: the weight tolerance
 SPEC_ATOL = 1e-12      # x the field's total: underflow-level terms (e.g. an absorption optical depth of
@@ -33,6 +35,24 @@ def trace_match(tr_o, tr_g):
         else:
             bad.add(i)
     return len(go), len(gg), match, bad
+
+
+def match_residuals(tr_o, tr_g):
+    """largest relative |w| and |e| differences over the photons whose discrete outcome (end reason,
+    bins, n_scatt, n_step within 1) agrees on both sides -- what W_RTOL / E_RTOL must cover"""
+    go = {int(r["id"]): r for r in tr_o}
+    mw = me = 0.0
+    for r in tr_g:
+        a = go.get(int(r["id"]))
+        if (a is None or a["end_reason"] != r["end_reason"] or a["ix2"] != r["ix2"] or a["i_e"] != r["i_e"]
+                or a["n_scatt"] != r["n_scatt"] or abs(int(a["n_step"]) - int(r["n_step"])) > 1):
+            continue
+        rel = []
+        for key in ("w", "e"):
+            x, y = float(a[key]), float(r[key])
+            rel.append(abs(x - y) / max(abs(x), abs(y)) if max(abs(x), abs(y)) > 0 else 0.0)
+        mw, me = max(mw, rel[0]), max(me, rel[1])
+    return mw, me
 
 
 def check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad):

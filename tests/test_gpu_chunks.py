@@ -1,0 +1,64 @@
+"""A pass fed to the engine in chunks (INTEGRATION.md path (a): the reference's emitter output handed
+over in batches of ~4 M photons) against the same pass in one call.
+
+The live-bias in-flight cap (GRM_OPT_FLIGHT_RATIO, grm_engine.hip run_transport) bounds the lanes of a
+call by the history the counters will hold -- the photons tracked since the reset plus the call's --
+so only the first chunks of a pass run on a reduced grid; from the second on the grid grows, and the
+last chunks run on the full grid, as the one-call pass does (the cap once counted the
+call's photons only, so every 4 M chunk ran on a third of the GPU).
+
+Asserted: every chunk's grid >= the one before, the last chunk's = the one-call grid; no photon lost;
+every primary tracked once; the chunked pass's counters and luminosity within the live bias's run-to-run
+spread of the one-call pass (recorded 4-6 % sd per run, L ~0.1 %).
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+CHUNK = 4 << 20
+
+
+def test_pass_in_chunks_reaches_full_grid(dump_dir):
+    import grmonty_amd as G
+    from grmonty_amd.synth_dump import ensure_dump
+    path = ensure_dump(os.path.join(dump_dir, "synth192.dump"), 192, 192)
+    model = G.Model.load(path, photon_n=1_000_000).init(8, device=0)
+    eng = G.Engine(model, device=0)
+    eng.emit_setup(model)
+    res = {}
+    for mode in ("one call", "chunks"):
+        eng.reset()
+        eng.set_option(G.OPT_SEED, 123)
+        eng.set_option(G.OPT_ID_BASE, 0)
+        p, n = eng.emit(seed=123)
+        t = time.time()
+        grids, prim = [], 0
+        if mode == "one call":
+            eng.track_device(p, n)
+            st = eng.stats()
+            grids.append(st["last_grid"])
+            prim = st["n_primaries"]
+        else:
+            for off in range(0, n, CHUNK):
+                k = min(CHUNK, n - off)
+                eng.track_device(p + off * G.INIT_PHOTON.itemsize, k)
+                st = eng.stats()
+                grids.append(st["last_grid"])
+                prim += st["n_primaries"]
+        spec, n_rec, n_scatt, _ = eng.finish()
+        st = eng.stats()
+        assert st["n_dropped"] == 0 and st["n_abandoned"] == 0
+        lum = model.write_spectrum(spec, None)["luminosity"]
+        res[mode] = dict(grids=grids, n=n, rec=n_rec, lum=lum, s=time.time() - t, prim=prim)
+        print(f"{mode}: {n} photons, grids {grids}, recorded {n_rec}, L {lum:.4f}, {time.time() - t:.3f} s")
+    eng.close()
+    a, b = res["one call"], res["chunks"]
+    assert b["prim"] == b["n"] == a["n"]
+    assert all(x <= y for x, y in zip(b["grids"], b["grids"][1:])), b["grids"]
+    assert b["grids"][-1] == a["grids"][0] and len(b["grids"]) >= 3
+    assert b["grids"][1] > b["grids"][0]
+    assert abs(b["rec"] / a["rec"] - 1) < 0.25
+    assert abs(b["lum"] / a["lum"] - 1) < 0.01

@@ -54,11 +54,14 @@ def test_grid512_photon_by_photon(dump512):
     spec_g = eng.finish()[0]
     st = eng.stats()
     assert st["n_dropped"] == 0 and st["n_primaries"] == len(sel)
-    from parity_util import MIN_MATCH, check_spectrum_cells, trace_match
+    from parity_util import E_RTOL, MIN_MATCH, W_RTOL, check_spectrum_cells, match_residuals, trace_match
     n_o, n_g, match, bad = trace_match(tr_o, tr_g)
     n_cmp, n_excl = check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad)
     print(f"512^2: oracle ends {n_o} device ends {n_g} matching {match / n_o:.4f}; spectrum cells compared "
           f"(12 fields) {n_cmp}, excluded {n_excl}")
+    mw, me = match_residuals(tr_o, tr_g)
+    print(f"512^2: largest relative differences of matching photons: w {mw:.3e} (bar {W_RTOL:g}), e {me:.3e} "
+          f"(bar {E_RTOL:g})")
     assert match / n_o >= MIN_MATCH
 
 

@@ -78,7 +78,7 @@ def test_photon_by_photon(setup, oracle64, lone):
         assert st["n_early"] == 0, st["n_early"]
     assert st["n_dropped"] == 0
     assert st["n_primaries"] == len(sel)
-    from parity_util import MIN_MATCH, check_spectrum_cells, trace_match
+    from parity_util import E_RTOL, MIN_MATCH, W_RTOL, check_spectrum_cells, match_residuals, trace_match
     gg = {int(r["id"]): r for r in tr_g}
     # primaries: every one of them ends exactly once on both sides
     assert all(i in gg for i in range(len(sel)))
@@ -88,6 +88,9 @@ def test_photon_by_photon(setup, oracle64, lone):
     n_cmp, n_excl = check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad)
     print(f"oracle ends {n_o} device ends {n_g} matching {frac_match:.4f}; spectrum cells compared "
           f"(12 fields) {n_cmp}, excluded {n_excl}")
+    mw, me = match_residuals(tr_o, tr_g)
+    print(f"largest relative differences of matching photons: w {mw:.3e} (bar {W_RTOL:g}), e {me:.3e} "
+          f"(bar {E_RTOL:g})")
     assert frac_match >= MIN_MATCH
     assert n_cmp >= 1200 - 12
 

@@ -7,6 +7,7 @@ profiles/pmc_traffic.json, which bench.py reports as roofline.traffic.
 """
 import csv
 import json
+import os
 import sys
 
 
@@ -32,6 +33,7 @@ out = {"bytes_per_dominant_launch": (2.0 * f_kb + w_kb) * 1024.0,
        "dominant_launches": k, "all_fetch_kb": fetch, "all_write_kb": write,
        "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) -- python3 bench.py --steps %d "
                   "--warmup %d --cpu-seconds 0 --overlap 0" % (bench["steps"], bench["warmup"]),
+       "source": "%s (tree %s)" % (sys.argv[4], os.environ.get("TREE_REV", "?")),
        "note": "the K+W largest track_kernel dispatches = one dominant launch per pass; bytes = 2 x FETCH_SIZE + "
                "WRITE_SIZE (KB -> B); the bench line of the FETCH run: " + steps}
 json.dump(out, open(sys.argv[4], "w"), indent=1)
