@@ -35,21 +35,20 @@ def test_pass_in_chunks_reaches_full_grid(dump_dir):
         eng.set_option(G.OPT_ID_BASE, 0)
         p, n = eng.emit(seed=123)
         t = time.time()
-        grids, prim = [], 0
+        grids = []
         if mode == "one call":
             eng.track_device(p, n)
             st = eng.stats()
             grids.append(st["last_grid"])
-            prim = st["n_primaries"]
         else:
             for off in range(0, n, CHUNK):
                 k = min(CHUNK, n - off)
                 eng.track_device(p + off * G.INIT_PHOTON.itemsize, k)
                 st = eng.stats()
                 grids.append(st["last_grid"])
-                prim += st["n_primaries"]
         spec, n_rec, n_scatt, _ = eng.finish()
         st = eng.stats()
+        prim = st["n_primaries"]  # since the reset
         assert st["n_dropped"] == 0 and st["n_abandoned"] == 0
         lum = model.write_spectrum(spec, None)["luminosity"]
         res[mode] = dict(grids=grids, n=n, rec=n_rec, lum=lum, s=time.time() - t, prim=prim)
