@@ -158,6 +158,9 @@ struct Ctl {
      * n_recorded and the max of max tau_scatt over the ranks' blocks of this pass. */
     const DevCounters *const *peers;
     int n_peers, ctr_slot;
+    /* split_kernel (grm_split.hip): an interaction wave runs its block once split_thr / 64 of its
+     * active lanes have a step ready, or after split_spin short sleeps */
+    int split_thr, split_spin;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -393,14 +396,20 @@ constexpr int SPEC_CELL = 16;                              /* padded slice cell 
 constexpr int SPEC_LDS = N_TH_BINS * N_E_BINS * SPEC_CELL; /* doubles per slice */
 __device__ __forceinline__ double *spec_slice(const Ctl &C) { return C.spec_blocks + (size_t)blockIdx.x * SPEC_LDS; }
 constexpr int RECBUF_N = 16, RECBUF_FLUSH = 8;
-__shared__ double s_recv[GRM_BLOCK / 64][RECBUF_N * SPEC_FIELDS]; /* per-wave record addends */
-__shared__ int s_recc[GRM_BLOCK / 64][RECBUF_N];                   /* their slice cells */
-__shared__ int s_recn[GRM_BLOCK / 64];                             /* records buffered */
-__shared__ unsigned long long s_cnt[BLOCK / 64][4]; /* n_recorded, n_scatt, max tau bits, max flushed */
+/* the waves that record (all of a track_kernel / lone workgroup; the interaction waves of the split
+ * kernel, grm_split.hip) and a wave's index among them */
+#ifndef GRM_REC_WAVES
+#define GRM_REC_WAVES (GRM_BLOCK / 64)
+#define GRM_REC_WAVE(t) ((t) >> 6)
+#endif
+__shared__ double s_recv[GRM_REC_WAVES][RECBUF_N * SPEC_FIELDS]; /* per-wave record addends */
+__shared__ int s_recc[GRM_REC_WAVES][RECBUF_N];                   /* their slice cells */
+__shared__ int s_recn[GRM_REC_WAVES];                             /* records buffered */
+__shared__ unsigned long long s_cnt[GRM_REC_WAVES][4]; /* n_recorded, n_scatt, max tau bits, max flushed */
 
 __device__ __forceinline__ void flush_counters(const Ctl &C) {
     if ((threadIdx.x & 63) == 0) {
-        unsigned long long *c = s_cnt[threadIdx.x >> 6];
+        unsigned long long *c = s_cnt[GRM_REC_WAVE(threadIdx.x)];
         if (c[0]) {
             atomicAdd(&C.ctr->n_recorded, c[0]);
             c[0] = 0;
@@ -425,7 +434,7 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
     int ix2 = -1, i_e = -1, reason = 1;
     const double e = cold->e;
     if (!(isnan(w) || isnan(e))) {
-        unsigned long long *cnt = s_cnt[threadIdx.x >> 6];
+        unsigned long long *cnt = s_cnt[GRM_REC_WAVE(threadIdx.x)];
         atomicMax(cnt + 2, (unsigned long long)__double_as_longlong(tau_scatt)); /* tau_scatt >= 0 */
         if (x2 < 0.5 * (P.xs2 + P.xe2))
             ix2 = (int)(x2 / P.th_dx2);
@@ -442,7 +451,7 @@ __device__ void record_photon(const Params &P, const Ctl &C, const Cold *cold, u
                 const double x1i = cold->x1i, x2i = cold->x2i;
                 int slot = RECBUF_N;
                 if (cell_stride == SPEC_CELL) {
-                    const int wv = threadIdx.x >> 6;
+                    const int wv = GRM_REC_WAVE(threadIdx.x);
                     slot = atomicAdd(&s_recn[wv], 1);
                     if (slot < RECBUF_N) {
                         double *b = &s_recv[wv][slot * SPEC_FIELDS];
@@ -498,7 +507,7 @@ __device__ __forceinline__ void end_of_life(const Params &P, const Ctl &C, const
 /* the wave's buffered records into the workgroup's slice: lane j adds field j % 12 of record j / 12
  * (called by the whole wave at a converged point) */
 __device__ __forceinline__ void flush_records(const Ctl &C) {
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = GRM_REC_WAVE(threadIdx.x), lane = threadIdx.x & 63;
     const int n = min(__builtin_amdgcn_readfirstlane(s_recn[wv]), RECBUF_N);
     double *slice = spec_slice(C);
     for (int j = lane; j < n * SPEC_FIELDS; j += 64) {
@@ -508,23 +517,23 @@ __device__ __forceinline__ void flush_records(const Ctl &C) {
     if (lane == 0) s_recn[wv] = 0;
 }
 
-/* emitted photon -> lane (harm_model.cpp:373-391) */
-__device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L, Cold *cold) {
+/* emitted photon -> lane (harm_model.cpp:373-391); n_scatt = 0 is the caller's */
+__device__ __forceinline__ void load_primary_core(const Ctl &C, uint64_t idx, Rng &rng, double x[4], double k[4],
+                                                  double &w, Cold *cold) {
     const double2 *s = reinterpret_cast<const double2 *>(reinterpret_cast<const grm_init_photon *>(C.pool) + idx);
     double2 v[7]; /* x, k, w, e, l, n_e_0, theta_e_0, b_0 (e_0 and n_scatt = 0 are not needed) */
 #pragma unroll
     for (int q = 0; q < 7; ++q) v[q] = s[q];
-    L.x[0] = v[0].x; L.x[1] = v[0].y; L.x[2] = v[1].x; L.x[3] = v[1].y;
-    L.k[0] = v[2].x; L.k[1] = v[2].y; L.k[2] = v[3].x; L.k[3] = v[3].y;
-    L.w = v[4].x;
-    L.n_scatt() = 0;
-    L.rng.id = C.id_base + idx;
-    L.rng.ctr = 0;
-    L.rng.ctr_hi = 0;
+    x[0] = v[0].x; x[1] = v[0].y; x[2] = v[1].x; x[3] = v[1].y;
+    k[0] = v[2].x; k[1] = v[2].y; k[2] = v[3].x; k[3] = v[3].y;
+    w = v[4].x;
+    rng.id = C.id_base + idx;
+    rng.ctr = 0;
+    rng.ctr_hi = 0;
     Cold c;
     c.e = v[4].y;
-    c.x1i = L.x[1];
-    c.x2i = L.x[2];
+    c.x1i = x[1];
+    c.x2i = x[2];
     c.n_e_0 = v[5].y;
     c.theta_e_0 = v[6].x;
     c.b_0 = v[6].y;
@@ -533,17 +542,22 @@ __device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L
     *cold = c;
 }
 
+__device__ __forceinline__ void load_primary(const Ctl &C, uint64_t idx, Lane &L, Cold *cold) {
+    load_primary_core(C, idx, L.rng, L.x, L.k, L.w, cold);
+    L.n_scatt() = 0;
+}
+
 /* scatter request -> child photon in the lane (scatter_super_photon after its first
  * validity check, harm_model.cpp:1083-1144, with sample_scattered_photon :1147-1215).
  * false = child invalid (k_tetrad out of range or NaN). */
-__device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane &L, Cold *cold) {
-    L.rng.id = R.id;
-    L.rng.ctr = 0;
-    L.rng.ctr_hi = 0;
-    L.w = R.w;
-    L.n_scatt() = R.n_scatt;
+__device__ __forceinline__ bool sample_child_core(const Params &P, const SReq &R, Rng &rng, double x[4], double k[4],
+                                                  double &w, Cold *cold) {
+    rng.id = R.id;
+    rng.ctr = 0;
+    rng.ctr_hi = 0;
+    w = R.w;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) L.x[i] = R.x[i];
+    for (int i = 0; i < 4; ++i) x[i] = R.x[i];
     Cold c;
     c.x1i = R.x[1];
     c.x2i = R.x[2];
@@ -577,11 +591,11 @@ __device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane 
     bool ok = !(kt[0] > 1.0e5 || kt[0] < 0.0 || isnan(kt[1]));
     if (ok) {
         double p[4], ktp[4];
-        sample_electron(L.rng, kt, p, R.theta_e);
-        sample_scattered(L.rng, kt, p, ktp);
+        sample_electron(rng, kt, p, R.theta_e);
+        sample_scattered(rng, kt, p, ktp);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) L.k[i] = ec[0][i] * ktp[0] + ec[1][i] * ktp[1] + ec[2][i] * ktp[2] + ec[3][i] * ktp[3];
-        ok = !isnan(L.k[1]);
+        for (int i = 0; i < 4; ++i) k[i] = ec[0][i] * ktp[0] + ec[1][i] * ktp[1] + ec[2][i] * ktp[2] + ec[3][i] * ktp[3];
+        ok = !isnan(k[1]);
         if (ok) {
             /* e_cov^T (-k0', k1', k2', k3'): only component 0 is needed (e; l enters no result) */
             ktp[0] = -ktp[0];
@@ -597,6 +611,11 @@ __device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane 
     }
     *cold = c;
     return ok;
+}
+
+__device__ bool sample_child(const Params &P, const Ctl &C, const SReq &R, Lane &L, Cold *cold) {
+    L.n_scatt() = R.n_scatt;
+    return sample_child_core(P, R, L.rng, L.x, L.k, L.w, cold);
 }
 
 __device__ __forceinline__ void load_sreq(const SReq *src, SReq &R) {
@@ -1666,7 +1685,7 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
 
 #endif /* GRM_LONE_TU */
 
-#ifndef GRM_LONE_TU
+#if !defined(GRM_LONE_TU) && !defined(GRM_SPLIT_TU)
 /* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
  * completed a step, the rest of the while-loop body of track_super_photon
  * (harm_model.cpp:919-1063).  A lane that has to halve its step (push_photon's recursion,
@@ -2394,15 +2413,18 @@ __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
         __threadfence_system();
     }
 }
-#endif /* !GRM_LONE_TU */
+#endif /* !GRM_LONE_TU && !GRM_SPLIT_TU */
 
 } /* namespace */
 
-#ifndef GRM_LONE_TU
+#if !defined(GRM_LONE_TU) && !defined(GRM_SPLIT_TU)
 /* lone_kernel / early_kernel live in grm_lone.hip (the same source, compiled without
  * -disable-machine-licm, see there); Params and Ctl cross as bytes */
 extern "C" hipError_t grm_lone_launch(int which, unsigned grid, hipStream_t s, const void *P, size_t p_size,
                                       const void *C, size_t c_size);
+/* split_kernel lives in grm_split.hip (the bulk transport with geometry and interaction waves) */
+extern "C" hipError_t grm_split_launch(unsigned grid, hipStream_t s, const void *P, size_t p_size, const void *C,
+                                       size_t c_size);
 
 /* ========================================================================= */
 /* engine object + C ABI                                                      */
@@ -2438,6 +2460,8 @@ struct grm_engine {
     uint64_t id_base = 0;
     int grid_override = 0;
     int64_t flight_ratio = 96; /* GRM_OPT_FLIGHT_RATIO: a live-bias call of n photons runs on <= n / this lanes */
+    int split = 0;             /* GRM_OPT_SPLIT: the bulk launch is split_kernel (grm_split.hip) */
+    int split_thr = 48, split_spin = 8; /* GRM_OPT_SPLIT_THR / _SPIN */
     double max_tau_init = 0.0;
     bool frozen_set = false;
     /* photons; -1 = lanes; -2 (default) = auto: lanes for a call of fewer than WARMUP_AUTO_RATIO x lanes
@@ -2665,6 +2689,8 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.lone_count = e->d_small + 7;
     C.lone_all = e->lone == 2;
     C.karg_test = e->karg_test;
+    C.split_thr = e->split_thr;
+    C.split_spin = e->split_spin;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
@@ -2790,8 +2816,12 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
          * round-robin, so with the worker's XCD full one bulk workgroup waits and starts (to find
          * the pool empty) as the bulk drains -- 255 run either way, and a full grid needs no guess
          * which XCD the worker lands on */
-        hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
-        HIPCHK(e, hipGetLastError());
+        if (e->split) {
+            HIPCHK(e, grm_split_launch((unsigned)grid, e->stream, &e->P, sizeof(Params), &C, sizeof(Ctl)));
+        } else {
+            hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
+            HIPCHK(e, hipGetLastError());
+        }
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
         /* the photons the launch handed over (a count on the device), one wave pair each; their
          * children join this launch's overflow pool */
@@ -3112,6 +3142,9 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
+    case GRM_OPT_SPLIT: e->split = v != 0; return 0;
+    case GRM_OPT_SPLIT_THR: e->split_thr = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
+    case GRM_OPT_SPLIT_SPIN: e->split_spin = v < 0 ? 0 : (v > 1 << 20 ? 1 << 20 : (int)v); return 0;
     case 18: case 20: case 21: e->err = "retired option " + std::to_string(opt); return -1;
     default: e->err = "unknown option"; return -1;
     }
@@ -3700,4 +3733,4 @@ size_t grm_sizeof(int which) {
 const char *grm_version(void) { return "grmonty_amd 0.1.0 (gfx950)"; }
 
 } /* extern "C" */
-#endif /* !GRM_LONE_TU */
+#endif /* !GRM_LONE_TU && !GRM_SPLIT_TU */

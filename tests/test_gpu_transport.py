@@ -38,16 +38,20 @@ def setup(model64, oracle64):
     return G, O, sel, snap, eng
 
 
-@pytest.mark.parametrize("lone", [1, 2, 3, 4], ids=["lane-loop", "lone-kernel", "early-worker", "early-serialised"])
+@pytest.mark.parametrize("lone", [1, 2, 3, 4, 5, 6],
+                         ids=["lane-loop", "lone-kernel", "early-worker", "early-serialised", "split", "split-early"])
 def test_photon_by_photon(setup, oracle64, lone):
     """lone=2 hands every photon to the lone-photon kernel (a two-wave pair per photon, halving walks
     over the lanes) at the top of its first step; lone=3 hands every photon that reaches 40 steps to
     the concurrent early worker (up to its queue's 1024); lone=4 runs that worker ahead of the main
-    launch on its stream, as a kernel-serialising profiler would, so it must leave and take none:
-    those paths against the oracle"""
+    launch on its stream, as a kernel-serialising profiler would, so it must leave and take none;
+    lone=5 runs the bulk as split_kernel (geometry and interaction waves, grm_split.hip), lone=6 that
+    kernel handing photons of 40 steps to the early worker: those paths against the oracle"""
     G, O, sel, snap, eng = setup
+    eng.set_option(G.OPT_SPLIT, 1 if lone >= 5 else 0)
+    eng.set_option(G.OPT_WATCHDOG_MS, 20000 if lone >= 5 else 60000)
     eng.set_option(G.OPT_LONE, 1 if lone >= 3 else lone)
-    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone >= 3 else 5000)
+    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone in (3, 4, 6) else 5000)
     eng.set_option(G.OPT_EARLY_SERIAL, 1 if lone == 4 else 0)
     oracle64.reset()
     tr_o = oracle64.track(sel, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=snap["scatt"],
@@ -70,9 +74,11 @@ def test_photon_by_photon(setup, oracle64, lone):
     eng.set_option(G.OPT_LONE, 1)
     eng.set_option(G.OPT_EARLY_STEPS, 5000)
     eng.set_option(G.OPT_EARLY_SERIAL, 0)
+    eng.set_option(G.OPT_SPLIT, 0)
+    eng.set_option(G.OPT_WATCHDOG_MS, 60000)
     if lone == 2:
         assert st["n_lone"] >= len(sel) // 2, st["n_lone"]
-    if lone == 3:
+    if lone in (3, 6):
         assert st["n_early"] >= 200, st["n_early"]
     if lone == 4:
         assert st["n_early"] == 0, st["n_early"]
