@@ -98,7 +98,7 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
     unsigned long long cur = 0;   /* the request in force */
     uint32_t gen = 0, q = 0;      /* q: the slot the next completed push goes to */
     int st = GS_IDLE;
-    bool setup = false;
+    bool setup = false, head = false; /* head: the push in progress is a generation's head (set-up or scattering point) */
     double dl = 0.0;
     int depth = 0;
     uint32_t pend = 0;
@@ -119,6 +119,7 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
             } else {
                 ring_load_state(slot_of(q + SP_R - 1), p, x, k, dk, e0s); /* photon_2 / the start state */
                 setup = kind == SK_NEW;
+                head = true;
                 dl = setup ? 0.0 : s_len[p];
                 depth = 0;
                 pend = 0;
@@ -222,8 +223,11 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 ++q;
-                /* a step ending outside [x1_min, x1_max] (or at NaN) ends the photon at its stop test */
-                st = (x[1] < P.x1_min || x[1] > P.x1_max || isnan(x[1])) ? GS_IDLE : GS_START;
+                /* a step ending outside [x1_min, x1_max] (or at NaN) ends the photon at its stop test
+                 * after the push (:932).  A head has no such test: the loop-top test (:919) of the step
+                 * after it ends the photon, so that step is pushed (and discarded) all the same */
+                st = (!head && (x[1] < P.x1_min || x[1] > P.x1_max || isnan(x[1]))) ? GS_IDLE : GS_START;
+                head = false;
             }
         }
     }
