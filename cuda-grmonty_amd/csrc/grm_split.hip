@@ -72,6 +72,17 @@ __shared__ unsigned s_cons[SP_PH];
 __shared__ int s_exit[SP_PAIRS];
 __shared__ int s_swtop[SP_PAIRS];
 
+/* diagnostic build (-DGRM_TIMING): wave-level accounting into Ctl.timing, slots 0-7 interaction waves
+ * (loop trips, evaluation rounds, ready lanes in them, active lanes in them, cycles in the evaluation,
+ * cycles in all, waiting trips, trips that refilled), 8-15 geometry waves (loop trips, trips with a
+ * push, pushing lanes, lanes held by a full ring, idle lanes, cycles in all, cycles in the push,
+ * idle trips) */
+#ifdef GRM_TIMING
+#define SP_T(v, x) (v) += (x)
+#else
+#define SP_T(v, x) do { } while (0)
+#endif
+
 __device__ __forceinline__ double &ring(int slot, int f, int p) { return s_ring[(slot * SP_F + f) * SP_PH + p]; }
 __device__ __forceinline__ int slot_of(uint32_t q) { return (int)(q % (uint32_t)SP_R); }
 
@@ -103,10 +114,15 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
     int depth = 0;
     uint32_t pend = 0;
     unsigned idle_spins = 0;
+#ifdef GRM_TIMING
+    unsigned long long tg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+#endif
     while (true) {
         KArgsK *const kt = karg_fresh(ka);
         const Params &P = karg_params(kt);
         ++trips;
+        SP_T(tg[0], 1);
         if (__hip_atomic_load(&s_exit[pair], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
         const unsigned long long r = __hip_atomic_load(&s_req[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (r != cur) {
@@ -129,6 +145,7 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
         if (st == GS_START) {
             /* photon_2 of the step is slot q - 1 (the last one written); slot q must be free */
             const uint32_t cons = __hip_atomic_load(&s_cons[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            SP_T(tg[3], (unsigned long long)__popcll(__ballot((int)(q - cons) > SP_R - 2)));
             if ((int)(q - cons) <= SP_R - 2) {
                 dl = step_size(P, x, k); /* :927, 1620-1630 */
                 depth = 0;
@@ -138,7 +155,9 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
             }
         }
         const bool push = st == GS_PUSH;
+        SP_T(tg[4], (unsigned long long)__popcll(__ballot(st == GS_IDLE)));
         if (!__ballot(push)) {
+            SP_T(tg[7], 1);
             if (idle_spins < 4)
                 __builtin_amdgcn_s_sleep(1);
             else
@@ -147,6 +166,11 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
             continue;
         }
         idle_spins = 0;
+        SP_T(tg[1], 1);
+        SP_T(tg[2], (unsigned long long)__popcll(__ballot(push)));
+#ifdef GRM_TIMING
+        const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
         if (push) {
             /* one attempt of push_photon at the current node of its halving tree (:1217-1289); the
              * set-up's attempt has zero length: x, k stay, dk = dk/dlambda at x (init_dkdlam) */
@@ -230,7 +254,17 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
                 head = false;
             }
         }
+#ifdef GRM_TIMING
+        tg[6] += __builtin_amdgcn_s_memtime() - tp0;
+#endif
     }
+#ifdef GRM_TIMING
+    tg[5] = __builtin_amdgcn_s_memtime() - tg0;
+    if ((threadIdx.x & 63) == 0) {
+        const Ctl &C = karg_ctl(karg_fresh(ka));
+        for (int i = 0; i < 8; ++i) atomicAdd(C.timing + 8 + i, tg[i]);
+    }
+#endif
 }
 
 /* ------------------------------------------------------------------------------------------- */
@@ -299,12 +333,17 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
     unsigned trip = 1;
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
     __hip_atomic_store(&s_cons[p], cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef GRM_TIMING
+    unsigned long long ti[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long ti0 = __builtin_amdgcn_s_memtime();
+#endif
 
     while (true) {
         KArgsK *const kt = karg_fresh(ka);
         const Params &P = karg_params(kt);
         const Ctl &C = karg_ctl(kt);
         ++wave_trips;
+        SP_T(ti[0], 1);
         if (warm && blockIdx.x >= WARM_BLOCKS) { /* the warm-up's batches go to the first workgroups */
             unsigned long long end = 0;
             if (lane_id == 0) end = __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -459,6 +498,7 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
                     }
                 }
                 if (lane_id == 0) *wtop = top - k_child;
+                SP_T(ti[7], (k_child + k_pool) > 0 ? 1 : 0);
                 bool has = false, ok = true;
                 double x[4], k[4];
                 if (!active && r < k_child) {
@@ -593,11 +633,18 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
             const int need = max(1, (n_act * C.split_thr) >> 6);
             if (n_ready == 0 || (n_ready < need && spins < (unsigned)C.split_spin)) {
                 ++spins;
+                SP_T(ti[6], 1);
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
             spins = 0;
+            SP_T(ti[1], 1);
+            SP_T(ti[2], (unsigned long long)n_ready);
+            SP_T(ti[3], (unsigned long long)n_act);
         }
+#ifdef GRM_TIMING
+        const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
         bool stepped = false;
         if (ready) {
             const double x1 = ring(sc, SF_X1, p);
@@ -762,6 +809,9 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
             }
         }
         __hip_atomic_store(&s_cons[p], cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef GRM_TIMING
+        ti[4] += __builtin_amdgcn_s_memtime() - tp0;
+#endif
         wave_steps += (unsigned long long)__popcll(__ballot(stepped));
         if (warm) {
             int d = flight;
@@ -771,6 +821,11 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
             flight = 0;
         }
     }
+#ifdef GRM_TIMING
+    ti[5] = __builtin_amdgcn_s_memtime() - ti0;
+    if (lane_id == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(C0.timing + i, ti[i]);
+#endif
     o_tracked = c_tracked;
     o_primaries = c_primaries;
     o_children = c_children;

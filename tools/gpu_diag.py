@@ -23,6 +23,13 @@ print(f"emit {len(ph)} photons {time.time() - t:.2f}s", flush=True)
 e = G.Engine(m, 0)
 if grid:
     e.set_option(G.OPT_GRID_BLOCKS, grid)
+if os.environ.get("SPLIT"):
+    e.set_option(G.OPT_SPLIT, int(os.environ["SPLIT"]))
+    print(f"split {os.environ['SPLIT']}", flush=True)
+for key, opt in (("SPLIT_THR", 24), ("SPLIT_SPIN", 25)):
+    if os.environ.get(key):
+        e.set_option(opt, int(os.environ[key]))
+        print(f"{key} {os.environ[key]}", flush=True)
 if os.environ.get("WARMUP"):
     e.set_option(G.OPT_WARMUP, int(os.environ["WARMUP"]))
     print(f"warmup {os.environ['WARMUP']}", flush=True)
@@ -85,6 +92,16 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
           f"bulk {st['last_steps'] / max(q[2], 1e-9) / 1e3:.4g} Msteps/s (steps / median wave exit)", flush=True)
     inst, tm = e.debug_timing(reset=True)
     if inst:
+        if os.environ.get("SPLIT"):
+            it, gt = tm[0:8], tm[8:16]
+            print(f"  split interaction waves: trips {it[0]}, rounds {it[1]} ({it[1] / max(it[0], 1):.3f} of trips), "
+                  f"ready lanes/round {it[2] / max(it[1], 1):.1f} of active {it[3] / max(it[1], 1):.1f}, cycles: "
+                  f"evaluation {it[4] / max(it[1], 1):.0f}/round = {it[4] / max(it[5], 1):.3f} of the loop, waiting trips "
+                  f"{it[6]}, refill trips {it[7]}", flush=True)
+            print(f"  split geometry waves: trips {gt[0]}, push trips {gt[1]}, pushing lanes/push trip "
+                  f"{gt[2] / max(gt[1], 1):.1f}, ring-full lanes/trip {gt[3] / max(gt[0], 1):.1f}, idle lanes/trip "
+                  f"{gt[4] / max(gt[0], 1):.1f}, push cycles/push trip {gt[6] / max(gt[1], 1):.0f} = "
+                  f"{gt[6] / max(gt[5], 1):.3f} of the loop, idle trips {gt[7]}", flush=True)
         tot = max(tm[3], 1)
         names = {0: "child", 1: "init", 2: "trip-tail", 7: "bias", 8: "phase0", 9: "attempt", 10: "restore",
                  11: "fluid", 12: "radiation", 13: "interact", 14: "refill-decision"}
