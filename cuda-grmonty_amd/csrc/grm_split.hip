@@ -156,14 +156,22 @@ __device__ void sp_geometry(KArgsK *ka, int pair, int p, unsigned long long &tri
         }
         const bool push = st == GS_PUSH;
         SP_T(tg[4], (unsigned long long)__popcll(__ballot(st == GS_IDLE)));
-        if (!__ballot(push)) {
-            SP_T(tg[7], 1);
-            if (idle_spins < 4)
-                __builtin_amdgcn_s_sleep(1);
-            else
-                __builtin_amdgcn_s_sleep(4);
-            ++idle_spins;
-            continue;
+        {
+            /* push once most live lanes can (an attempt issues the same instructions for 1 lane as for
+             * 64, and they are issue slots the interaction wave on this SIMD does not get), or after a
+             * few sleeps */
+            const int n_push = __popcll(__ballot(push));
+            const int n_live = __popcll(__ballot(st != GS_IDLE));
+            const Ctl &C = karg_ctl(kt);
+            if (n_push == 0 || (n_push < ((n_live * C.split_gthr) >> 6) && idle_spins < (unsigned)C.split_spin)) {
+                SP_T(tg[7], 1);
+                if (n_push || idle_spins < 4)
+                    __builtin_amdgcn_s_sleep(1);
+                else
+                    __builtin_amdgcn_s_sleep(4);
+                ++idle_spins;
+                continue;
+            }
         }
         idle_spins = 0;
         SP_T(tg[1], 1);
