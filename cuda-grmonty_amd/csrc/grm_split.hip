@@ -343,6 +343,7 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
     __hip_atomic_store(&s_cons[p], cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef GRM_TIMING
     unsigned long long ti[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tj[4] = {0, 0, 0, 0}; /* evaluation: to the fluid, fluid, radiation, the rest */
     const unsigned long long ti0 = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -689,11 +690,21 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
                 T.cth = ring(sc, SF_CTH, p);
                 Gcov G;
                 gcov_from_trig(P, T, G);
+#ifdef GRM_TIMING
+                const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
+#endif
                 ZoneFetch Z;
                 zone_fetch(P, xv, Z);
                 Fluid F;
                 fluid_from(P, xv, G, Z, F);
                 fl_ne = F.n_e;
+#ifdef GRM_TIMING
+                const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
+                if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+                    tj[0] += tq0 - tp0;
+                    tj[1] += tq1 - tq0;
+                }
+#endif
                 const bool at_sp = expect == E_SP, setup = expect == E_SETUP;
                 if (at_sp && F.n_e > 0.0 && (kv[0] > 1.0e5 || kv[0] < 0.0 || isnan(kv[0]) || isnan(kv[1]) || isnan(kv[3]))) {
                     w = 0.0; /* scatter_super_photon's parent-side check (:1076-1081) */
@@ -705,6 +716,10 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
                     double a_s = 0.0, a_a = 0.0;
                     if (!zero) radiation_coeffs(P, kv, F, nu, a_s, a_a);
                     const double bf = (zero && !at_sp) ? 0.0 : bias_func(bias_d, F.theta_e, w);
+#ifdef GRM_TIMING
+                    if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
+                        tj[2] += __builtin_amdgcn_s_memtime() - tq1;
+#endif
                     if (setup) {
                         a_si = a_s;
                         a_ai = a_a;
@@ -833,6 +848,12 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
     ti[5] = __builtin_amdgcn_s_memtime() - ti0;
     if (lane_id == 0)
         for (int i = 0; i < 8; ++i) atomicAdd(C0.timing + i, ti[i]);
+    /* the per-phase sums were kept by varying first lanes: reduce them over the wave */
+    for (int i = 0; i < 3; ++i) {
+        unsigned long long v = tj[i];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane_id == 0) atomicAdd(C0.timing + 44 + i, v);
+    }
 #endif
     o_tracked = c_tracked;
     o_primaries = c_primaries;
