@@ -162,6 +162,7 @@ struct Ctl {
      * active lanes have a step ready, or after split_spin short sleeps */
     int split_thr, split_spin;
     int split_gthr; /* a geometry wave pushes once split_gthr / 64 of its live lanes can (or after split_spin sleeps) */
+    int split_mode; /* 1: waves 0-3 geometry, 4-7 interaction; 2: roles by the SIMD a wave runs on */
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -2693,6 +2694,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.split_thr = e->split_thr;
     C.split_spin = e->split_spin;
     C.split_gthr = e->split_gthr;
+    C.split_mode = e->split;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
@@ -3144,7 +3146,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
-    case GRM_OPT_SPLIT: e->split = v != 0; return 0;
+    case GRM_OPT_SPLIT: e->split = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_SPLIT_THR: e->split_thr = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_SPLIT_SPIN: e->split_spin = v < 0 ? 0 : (v > 1 << 20 ? 1 << 20 : (int)v); return 0;
     case GRM_OPT_SPLIT_GTHR: e->split_gthr = v < 0 ? 0 : (v > 64 ? 64 : (int)v); return 0;

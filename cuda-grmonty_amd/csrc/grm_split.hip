@@ -42,9 +42,11 @@
  * (tests/test_gpu_transport.py[split]).
  */
 #define GRM_SPLIT_TU 1
-/* only the interaction waves record: four record buffers per workgroup, indexed by pair */
+/* only the interaction waves record: four record buffers per workgroup, indexed by the wave's pair */
+#include <hip/hip_runtime.h>
+__shared__ int s_recidx[8]; /* wave -> its pair (interaction waves) */
 #define GRM_REC_WAVES 4
-#define GRM_REC_WAVE(t) (((t) >> 6) & 3)
+#define GRM_REC_WAVE(t) (s_recidx[(t) >> 6])
 #include "grm_engine.hip"
 
 namespace {
@@ -71,6 +73,7 @@ __shared__ double s_len[SP_PH];             /* SCATTER: the re-push length dl * 
 __shared__ unsigned s_cons[SP_PH];
 __shared__ int s_exit[SP_PAIRS];
 __shared__ int s_swtop[SP_PAIRS];
+__shared__ int s_simd[SP_BLOCK / 64];
 
 /* diagnostic build (-DGRM_TIMING): wave-level accounting into Ctl.timing, slots 0-7 interaction waves
  * (loop trips, evaluation rounds, ready lanes in them, active lanes in them, cycles in the evaluation,
@@ -315,7 +318,7 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
                                unsigned &o_primaries, unsigned &o_children, unsigned &o_nstep_max, unsigned &o_long) {
     const unsigned lane_id = threadIdx.x & 63;
     const uint64_t gtid = (uint64_t)blockIdx.x * SP_BLOCK + threadIdx.x;
-    SReq *wstack = C0.stack + (gtid >> 6) * WSTACK_CAP;
+    SReq *wstack = C0.stack + (gtid >> 6) * WSTACK_CAP; /* the wave's own (allocated for every wave) */
     int *wtop = &s_swtop[pair];
     Cold *cold = C0.cold + gtid;
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
@@ -868,10 +871,35 @@ __global__ __launch_bounds__(SP_BLOCK, 1) void split_kernel(Params P_, Ctl C_) {
     const Params &P0 = P_;
     const int wave = threadIdx.x >> 6;
     const unsigned lane_id = threadIdx.x & 63;
-    const int pair = wave & (SP_PAIRS - 1);
+    /* Roles.  split 1: waves 0-3 geometry, 4-7 interaction (pair g = waves g, g + 4: the same SIMD when
+     * the waves are dealt round-robin).  split 2: by the SIMD each wave runs on (HW_ID), the geometry
+     * waves on SIMDs 0-1 and the interaction waves on SIMDs 2-3, two of a kind per SIMD (one wave's
+     * latency covered by the other's work of the same kind); pair g = the g-th wave of each role;
+     * a placement other than two waves per SIMD falls back to split 1. */
+    int pair = wave & (SP_PAIRS - 1);
+    bool geo = wave < SP_PAIRS;
+    if (C0.split_mode == 2) {
+        unsigned simd;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 4, 2)" : "=s"(simd));
+        if (lane_id == 0) s_simd[wave] = (int)simd;
+        __syncthreads();
+        int n_geo = 0, rank = 0, per[4] = {0, 0, 0, 0};
+        const bool g = simd < 2;
+        for (int v = 0; v < SP_BLOCK / 64; ++v) {
+            const int sv = s_simd[v] & 3;
+            ++per[sv];
+            n_geo += sv < 2 ? 1 : 0;
+            if (v < wave && (sv < 2) == g) ++rank;
+        }
+        if (n_geo == SP_PAIRS && per[0] == 2 && per[1] == 2 && per[2] == 2 && per[3] == 2) {
+            geo = g;
+            pair = rank;
+        }
+    }
     const int p = pair * 64 + (int)lane_id;
-    const bool geo = wave < SP_PAIRS;
     const uint64_t gtid = (uint64_t)blockIdx.x * SP_BLOCK + threadIdx.x;
+    if (lane_id == 0) s_recidx[wave] = pair;
+    __syncthreads();
     /* ring tags and requests start empty (generation 0 is never requested: the first is 1) */
     for (int i = threadIdx.x; i < SP_R * SP_PH; i += SP_BLOCK) s_tag[i] = ~0ull;
     if (threadIdx.x < SP_PH) {
