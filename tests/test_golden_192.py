@@ -61,7 +61,7 @@ def test_lag_emulator_fixture():
     from spectrum_stats import welch_z
     emu = json.load(open(os.path.join(HERE, "golden", "lag_emulator_synth192_pn1e5.json")))
     ora = json.load(open(os.path.join(HERE, "golden", "oracle_synth192_pn1e5.json")))["runs"]
-    for cfg in ("serial", "device"):
+    for cfg in ("serial", "device", "device_cap"):
         runs = [r for r in emu["runs"] if r["config"] == cfg]
         assert len(runs) >= 20
         for k in ("recorded", "scattered", "steps", "luminosity"):
