@@ -14,6 +14,7 @@ import json
 import os
 import sys
 import threading
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(os.path.dirname(HERE), "cuda-grmonty_amd"), HERE]
@@ -78,16 +79,19 @@ def main():
                 err.append(repr(ex))
                 go.abort()
 
+        wall = None
         if args.sequential:  # each rank's pass alone, in rank order (no barrier)
             go = threading.Barrier(1)
             for r in range(world):
                 rank(r)
         else:
             th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+            t0 = time.time()
             for t in th:
                 t.start()
             for t in th:
                 t.join()
+            wall = time.time() - t0
         if err:
             raise RuntimeError(err[0])
         spec = out[0]["spec"].copy()
@@ -96,6 +100,7 @@ def main():
                 spec[f] += o["spec"][f]
         job = {k: int(sum(o[k] for o in out)) for k in ("created", "recorded", "scattered", "steps")}
         job["luminosity"] = model.write_spectrum(spec, None)["luminosity"]
+        job["wall_s"] = wall  # the ranks' passes, emission to read-back (concurrent runs only)
         # every rank's view of the job's counters once all passes ended (the kernels' bias_den path):
         # must be the sums of the ranks' own counters and the max of their max tau_scatt
         job["max_tau"] = max(o["max_tau"] for o in out)
