@@ -795,7 +795,21 @@ __device__ __forceinline__ int walk_push(const Params &P, double x[4], double k[
                                          double hlen, int depth, uint32_t pend, int rank, int owner) {
     int rounds = 0; /* attempt rounds (diagnostics) */
     while (true) {
-        if (!(x[1] < P.xs1)) {
+        if (!(x[1] < P.xs1) && depth == MAX_SUBDIV) {
+            /* a leaf of the deepest level is accepted whatever its checks say (:1279): every lane makes
+             * that one attempt from the identical state, so no lane has to win and be broadcast (the
+             * second halves at depth MAX_SUBDIV -- every other round of a photon that halves to full
+             * depth, seed 124's tail in round 4) */
+            double e_1;
+            Trig T;
+            Gcov G;
+            if (QUAD)
+                push_attempt_quad(P, x, k, dk, e_0_s, ldexp(hlen, -MAX_SUBDIV), e_1, T, G, (int)(threadIdx.x & 3));
+            else
+                push_attempt(P, x, k, dk, e_0_s, ldexp(hlen, -MAX_SUBDIV), e_1, T, G);
+            e_0_s = e_1;
+            ++rounds;
+        } else if (!(x[1] < P.xs1)) {
             /* every lane attempts in place from the same start state; the winner's result is then
              * broadcast over all of them */
             const int d = depth + rank;
