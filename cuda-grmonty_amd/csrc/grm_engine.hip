@@ -1058,6 +1058,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
         cons = p;
         unpack13(pr.ctl.rs, x, k, dk, e_0_s);
     }
+    const double *ph2src = pr.ctl.rs; /* where the current step's start state (photon_2) is kept */
 #ifdef GRM_TIMING
     unsigned long long g_last = __builtin_amdgcn_s_memtime();
     unsigned long long tg[6] = {0, 0, 0, 0, 0, 0}; /* steps, rounds, walk, step size, rest, halved */
@@ -1096,13 +1097,6 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
             if (!spec) {
                 bool fail = false;
                 if (!(x[1] < P.xs1)) {
-                    double xb[4], kb[4], dkb[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        xb[i] = x[i];
-                        kb[i] = k[i];
-                        dkb[i] = dk[i];
-                    }
                     double e_1;
                     Trig T;
                     Gcov G;
@@ -1110,12 +1104,11 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
                     fail = GEO_QUAD ? push_attempt_quad(P, x, k, dk, e_0_s, dl, e_1, T, G, lane & 3)
                                     : push_attempt(P, x, k, dk, e_0_s, dl, e_1, T, G);
                     if (fail) { /* depth 0 failed: the serial walk goes on at depth 1 (:1279-1285) */
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            x[i] = xb[i];
-                            k[i] = kb[i];
-                            dk[i] = dkb[i];
-                        }
+                        /* from the step's start state, photon_2: the slot published last (or the
+                         * generation's restart state) -- no register copy on every step for the ~2 %
+                         * that fail (the copy cost ~24 moves per step of the serial chain) */
+                        double e_r;
+                        unpack13(ph2src, x, k, dk, e_r);
                         rounds += walk_push<GEO_QUAD>(P, x, k, dk, e_0_s, dl, 1, 2u, GEO_QUAD ? lane >> 2 : lane, 0);
                     } else {
                         e_0_s = e_1;
@@ -1143,6 +1136,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
             p = req & 0xffffffffull;
             cons = p; /* what the interaction wave has consumed when it requests a restart at p */
             unpack13(pr.ctl.rs, x, k, dk, e_0_s);
+            ph2src = pr.ctl.rs;
             spec = false;
             continue;
         }
@@ -1166,6 +1160,7 @@ __device__ void lone_geometry(const Params &P_, const Ctl &C, int lane, LonePair
             __hip_atomic_store(&S.tag, ((unsigned long long)gen << 32) | (p + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        ph2src = pr.ring[p % LONE_RING].out; /* lane 0's stores precede this wave's later loads */
         ++p;
     }
 }
