@@ -22,11 +22,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("jobs", nargs="+")
     ap.add_argument("--photon-n", type=float, default=1e6)
+    ap.add_argument("--pool", action="store_true", help="the files' jobs as one sample")
     a = ap.parse_args()
     tag = "pn1e6" if a.photon_n >= 1e6 else "pn1e5"
     o = json.load(open(os.path.join(REPO, "tests", "golden", f"oracle_synth192_{tag}.json")))["runs"]
-    for path in a.jobs:
-        jobs = json.load(open(path))
+    sets = [(p, json.load(open(p))) for p in a.jobs]
+    if a.pool:
+        sets = [(" + ".join(a.jobs), [j for _, js in sets for j in js])]
+    for path, jobs in sets:
         print(f"{path}: {len(jobs)} jobs vs {len(o)} oracle runs")
         for k in KEYS:
             dev = np.array([j[k] for j in jobs], dtype=np.float64)

@@ -15,5 +15,5 @@ for r in 1 2; do
   done
 done
 for s in auto 1; do
-  python tools/emu_vs_oracle.py gpurun_out/${T}_slack${s}_1.json gpurun_out/${T}_slack${s}_2.json --photon-n 1e6
+  python tools/emu_vs_oracle.py gpurun_out/${T}_slack${s}_1.json gpurun_out/${T}_slack${s}_2.json --photon-n 1e6 --pool
 done
