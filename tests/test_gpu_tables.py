@@ -10,7 +10,10 @@ agrees to 1e-13 (measured ~4e-15: the device's trapezoid e^x K2(x) and std::cyl_
 dndlnu_max, sums of 200 interpolated emissivities over a weight table that itself comes from the
 device K2, to 1e-11 (measured ~7e-13).  hotcross: most entries bit-identical; the Klein-Nishina
 expression (hotcross.cpp:144-151) cancels ~6 digits just above its w = 1e-3 switch, where a last-bit
-difference of log(1 + 2w) becomes ~1e-10 of sigma in both builds, so |d log10 sigma| <= 1e-9."""
+difference of log(1 + 2w) becomes ~1e-10 of sigma in both builds, so |d log10 sigma| <= 1e-9 (measured
+2.14e-10 at entry (111, 0), w = 1.2e-3, theta_e = 1e-4; the builder compiled without FMA contraction
+gives the same table bit for bit, profiles/r05_split/r05g_tables.log: the difference is ocml's vs
+glibc's last bits of log, which only a port of glibc's log would remove)."""
 import numpy as np
 import pytest
 
