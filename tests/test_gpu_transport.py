@@ -38,17 +38,19 @@ def setup(model64, oracle64):
     return G, O, sel, snap, eng
 
 
-@pytest.mark.parametrize("lone", [1, 2, 3, 4, 5, 6],
-                         ids=["lane-loop", "lone-kernel", "early-worker", "early-serialised", "split", "split-early"])
+@pytest.mark.parametrize("lone", [1, 2, 3, 4, 5, 6, 7],
+                         ids=["lane-loop", "lone-kernel", "early-worker", "early-serialised", "split", "split-early",
+                              "split-by-simd"])
 def test_photon_by_photon(setup, oracle64, lone):
     """lone=2 hands every photon to the lone-photon kernel (a two-wave pair per photon, halving walks
     over the lanes) at the top of its first step; lone=3 hands every photon that reaches 40 steps to
     the concurrent early worker (up to its queue's 1024); lone=4 runs that worker ahead of the main
     launch on its stream, as a kernel-serialising profiler would, so it must leave and take none;
     lone=5 runs the bulk as split_kernel (geometry and interaction waves, grm_split.hip), lone=6 that
-    kernel handing photons of 40 steps to the early worker: those paths against the oracle"""
+    kernel handing photons of 40 steps to the early worker, lone=7 that kernel with the roles dealt by
+    SIMD (GRM_OPT_SPLIT = 2): those paths against the oracle"""
     G, O, sel, snap, eng = setup
-    eng.set_option(G.OPT_SPLIT, 1 if lone >= 5 else 0)
+    eng.set_option(G.OPT_SPLIT, 2 if lone == 7 else (1 if lone >= 5 else 0))
     eng.set_option(G.OPT_WATCHDOG_MS, 20000 if lone >= 5 else 60000)
     eng.set_option(G.OPT_LONE, 1 if lone >= 3 else lone)
     eng.set_option(G.OPT_EARLY_STEPS, 40 if lone in (3, 4, 6) else 5000)
