@@ -1,4 +1,4 @@
-"""Sum rocprofv3 --pmc CSVs (gpurun_out/pmc_<tag>_<i>/run_counter_collection.csv) over track_kernel
+"""Sum rocprofv3 --pmc CSVs (gpurun_out/pmc_<tag>_<i>/run_counter_collection.csv) over track_kernel (or split_kernel)
 dispatches and print the derived ratios used in DESIGN.md §8."""
 import collections
 import csv
@@ -11,7 +11,7 @@ root, tag = sys.argv[1], sys.argv[2]
 tot = collections.defaultdict(float)
 for f in sorted(glob.glob(os.path.join(root, f"pmc_{tag}_*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        if "track_kernel" in r["Kernel_Name"]:
+        if "track_kernel" in r["Kernel_Name"] or "split_kernel" in r["Kernel_Name"]:
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
 steps = None
 for f in sorted(glob.glob(os.path.join(root, f"pmc_{tag}_*.log"))):
