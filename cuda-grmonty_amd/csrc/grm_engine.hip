@@ -2472,7 +2472,7 @@ struct grm_engine {
     int grid_override = 0;
     int64_t flight_ratio = 96; /* GRM_OPT_FLIGHT_RATIO: a live-bias call of n photons runs on <= n / this lanes */
     int split = 0;             /* GRM_OPT_SPLIT: the bulk launch is split_kernel (grm_split.hip) */
-    int split_thr = 48, split_spin = 8, split_gthr = 40; /* GRM_OPT_SPLIT_THR / _SPIN / _GTHR */
+    int split_thr = 48, split_spin = 4, split_gthr = 24; /* GRM_OPT_SPLIT_THR / _SPIN / _GTHR (profiles/r05_split) */
     double max_tau_init = 0.0;
     bool frozen_set = false;
     /* photons; -1 = lanes; -2 (default) = auto: lanes for a call of fewer than WARMUP_AUTO_RATIO x lanes

@@ -196,11 +196,11 @@ enum {
      * split_kernel (geometry waves push, interaction waves evaluate) */
     GRM_OPT_SPLIT = 23,
     /* split_kernel: an interaction wave evaluates its ready steps once this many 64ths of its active
-     * lanes have one (default 48), or after GRM_OPT_SPLIT_SPIN short sleeps (default 8) */
+     * lanes have one (default 48), or after GRM_OPT_SPLIT_SPIN short sleeps (default 4) */
     GRM_OPT_SPLIT_THR = 24,
     GRM_OPT_SPLIT_SPIN = 25,
     /* split_kernel: a geometry wave makes its push attempts once this many 64ths of its live lanes
-     * can (default 40), or after GRM_OPT_SPLIT_SPIN sleeps */
+     * can (default 24), or after GRM_OPT_SPLIT_SPIN sleeps */
     GRM_OPT_SPLIT_GTHR = 26
 };
 
