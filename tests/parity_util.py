@@ -39,21 +39,26 @@ def trace_match(tr_o, tr_g):
     return len(go), len(gg), match, bad
 
 
-def match_residuals(tr_o, tr_g):
+def match_residuals(tr_o, tr_g, steps=None):
     """largest relative |w| and |e| differences over the photons whose discrete outcome (end reason,
-    bins, n_scatt, n_step within 1) agrees on both sides -- what W_RTOL / E_RTOL must cover"""
+    bins, n_scatt, n_step within 1) agrees on both sides -- what W_RTOL / E_RTOL must cover; with
+    `steps` (a dict) also the count of those photons whose n_step differs (the +-1 allowance)"""
     go = {int(r["id"]): r for r in tr_o}
     mw = me = 0.0
+    n_step_off = 0
     for r in tr_g:
         a = go.get(int(r["id"]))
         if (a is None or a["end_reason"] != r["end_reason"] or a["ix2"] != r["ix2"] or a["i_e"] != r["i_e"]
                 or a["n_scatt"] != r["n_scatt"] or abs(int(a["n_step"]) - int(r["n_step"])) > 1):
             continue
+        n_step_off += int(a["n_step"]) != int(r["n_step"])
         rel = []
         for key in ("w", "e"):
             x, y = float(a[key]), float(r[key])
             rel.append(abs(x - y) / max(abs(x), abs(y)) if max(abs(x), abs(y)) > 0 else 0.0)
         mw, me = max(mw, rel[0]), max(me, rel[1])
+    if steps is not None:
+        steps["n_step_off_by_one"] = n_step_off
     return mw, me
 
 

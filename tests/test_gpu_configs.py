@@ -59,9 +59,10 @@ def test_grid512_photon_by_photon(dump512):
     n_cmp, n_excl = check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad)
     print(f"512^2: oracle ends {n_o} device ends {n_g} matching {match / n_o:.4f}; spectrum cells compared "
           f"(12 fields) {n_cmp}, excluded {n_excl}")
-    mw, me = match_residuals(tr_o, tr_g)
+    nst = {}
+    mw, me = match_residuals(tr_o, tr_g, nst)
     print(f"512^2: largest relative differences of matching photons: w {mw:.3e} (bar {W_RTOL:g}), e {me:.3e} "
-          f"(bar {E_RTOL:g})")
+          f"(bar {E_RTOL:g}); n_step off by one: {nst['n_step_off_by_one']}")
     assert match / n_o >= MIN_MATCH
 
 

@@ -96,9 +96,10 @@ def test_photon_by_photon(setup, oracle64, lone):
     n_cmp, n_excl = check_spectrum_cells(spec_o, spec_g, tr_o, tr_g, bad)
     print(f"oracle ends {n_o} device ends {n_g} matching {frac_match:.4f}; spectrum cells compared "
           f"(12 fields) {n_cmp}, excluded {n_excl}")
-    mw, me = match_residuals(tr_o, tr_g)
+    nst = {}
+    mw, me = match_residuals(tr_o, tr_g, nst)
     print(f"largest relative differences of matching photons: w {mw:.3e} (bar {W_RTOL:g}), e {me:.3e} "
-          f"(bar {E_RTOL:g})")
+          f"(bar {E_RTOL:g}); n_step off by one: {nst['n_step_off_by_one']}")
     assert frac_match >= MIN_MATCH
     assert n_cmp >= 1200 - 12
 
