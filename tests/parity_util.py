@@ -1,7 +1,8 @@
 """Photon-by-photon parity helpers shared by the GPU parity tests (device vs oracle, same emitted
 photons, same Philox streams, bias frozen at the same snapshot).
 
-A photon matches when its end reason, theta/energy bin, scattering count and step count agree and
+A photon matches when its end reason, theta/energy bin, scattering count and step count agree (the
+step count exactly: round 5 measured no photon off by one step on any path, r05m) and
 its weight and energy agree to rounding (device FMA / OCML vs glibc).  A photon whose rejection or
 sub-stepping decision flips on a last-bit difference diverges, and so do its children; such
 photons are counted (MIN_MATCH bounds them) and the spectrum cells they reach on either side are
@@ -31,7 +32,7 @@ def trace_match(tr_o, tr_g):
     for i in set(go) | set(gg):
         a, b = go.get(i), gg.get(i)
         if (a is not None and b is not None and a["end_reason"] == b["end_reason"] and a["ix2"] == b["ix2"]
-                and a["i_e"] == b["i_e"] and a["n_scatt"] == b["n_scatt"] and abs(int(a["n_step"]) - int(b["n_step"])) <= 1
+                and a["i_e"] == b["i_e"] and a["n_scatt"] == b["n_scatt"] and int(a["n_step"]) == int(b["n_step"])
                 and np.isclose(a["w"], b["w"], rtol=W_RTOL, atol=0) and np.isclose(a["e"], b["e"], rtol=E_RTOL)):
             match += 1
         else:
