@@ -347,6 +347,7 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
 #ifdef GRM_TIMING
     unsigned long long ti[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tj[4] = {0, 0, 0, 0}; /* evaluation: to the fluid, fluid, radiation, the rest */
+    unsigned long long tk[3] = {0, 0, 0};    /* loop top + refill, hand-overs, readiness (all trips) */
     const unsigned long long ti0 = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -356,6 +357,9 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
         const Ctl &C = karg_ctl(kt);
         ++wave_trips;
         SP_T(ti[0], 1);
+#ifdef GRM_TIMING
+        const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
+#endif
         if (warm && blockIdx.x >= WARM_BLOCKS) { /* the warm-up's batches go to the first workgroups */
             unsigned long long end = 0;
             if (lane_id == 0) end = __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -574,6 +578,10 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
                 }
             }
         }
+#ifdef GRM_TIMING
+        const unsigned long long tl1 = __builtin_amdgcn_s_memtime();
+        tk[0] += tl1 - tl0; /* loop top: refresh, record flush, refill */
+#endif
         if (!__any(active)) {
             if (warm) {
                 int d = flight;
@@ -633,6 +641,10 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
                 }
             }
         }
+#ifdef GRM_TIMING
+        const unsigned long long tl2 = __builtin_amdgcn_s_memtime();
+        tk[1] += tl2 - tl1; /* hand-overs */
+#endif
         /* the steps ready: wait until most active lanes have one (the block then issues with nearly
          * every lane), or a few sleeps */
         const int sc = slot_of(cons);
@@ -643,6 +655,9 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
             const int n_ready = __popcll(__ballot(ready));
             const int n_act = __popcll(__ballot(active));
             const int need = max(1, (n_act * C.split_thr) >> 6);
+#ifdef GRM_TIMING
+            tk[2] += __builtin_amdgcn_s_memtime() - tl2; /* readiness */
+#endif
             if (n_ready == 0 || (n_ready < need && spins < (unsigned)C.split_spin)) {
                 ++spins;
                 SP_T(ti[6], 1);
@@ -857,6 +872,8 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if (lane_id == 0) atomicAdd(C0.timing + 44 + i, v);
     }
+    if (lane_id == 0)
+        for (int i = 0; i < 3; ++i) atomicAdd(C0.timing + 32 + i, tk[i]);
 #endif
     o_tracked = c_tracked;
     o_primaries = c_primaries;

@@ -98,7 +98,9 @@ for rep in range(int(os.environ.get('DIAG_REPS', '3'))):
                   f"ready lanes/round {it[2] / max(it[1], 1):.1f} of active {it[3] / max(it[1], 1):.1f}, cycles: "
                   f"evaluation {it[4] / max(it[1], 1):.0f}/round = {it[4] / max(it[5], 1):.3f} of the loop, waiting trips "
                   f"{it[6]}, refill trips {it[7]}; per round: to the fluid {tm[44] / max(it[1], 1):.0f}, gather+fluid "
-                  f"{tm[45] / max(it[1], 1):.0f}, radiation+bias {tm[46] / max(it[1], 1):.0f} cycles", flush=True)
+                  f"{tm[45] / max(it[1], 1):.0f}, radiation+bias {tm[46] / max(it[1], 1):.0f} cycles; per trip: loop top + "
+                  f"refill {tm[32] / max(it[0], 1):.0f}, hand-overs {tm[33] / max(it[0], 1):.0f}, readiness "
+                  f"{tm[34] / max(it[0], 1):.0f} cycles", flush=True)
             print(f"  split geometry waves: trips {gt[0]}, push trips {gt[1]}, pushing lanes/push trip "
                   f"{gt[2] / max(gt[1], 1):.1f}, ring-full lanes/trip {gt[3] / max(gt[0], 1):.1f}, idle lanes/trip "
                   f"{gt[4] / max(gt[0], 1):.1f}, push cycles/push trip {gt[6] / max(gt[1], 1):.0f} = "
