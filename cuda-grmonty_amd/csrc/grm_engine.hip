@@ -163,6 +163,7 @@ struct Ctl {
     int split_thr, split_spin;
     int split_gthr; /* a geometry wave pushes once split_gthr / 64 of its live lanes can (or after split_spin sleeps) */
     int split_mode; /* 1: waves 0-3 geometry, 4-7 interaction; 2: roles by the SIMD a wave runs on */
+    int split_batch; /* consecutive ready slots an interaction lane may evaluate per round */
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -2473,6 +2474,7 @@ struct grm_engine {
     int64_t flight_ratio = 96; /* GRM_OPT_FLIGHT_RATIO: a live-bias call of n photons runs on <= n / this lanes */
     int split = 0;             /* GRM_OPT_SPLIT: the bulk launch is split_kernel (grm_split.hip) */
     int split_thr = 48, split_spin = 4, split_gthr = 24; /* GRM_OPT_SPLIT_THR / _SPIN / _GTHR (profiles/r05_split) */
+    int split_batch = 1; /* GRM_OPT_SPLIT_BATCH */
     double max_tau_init = 0.0;
     bool frozen_set = false;
     /* photons; -1 = lanes; -2 (default) = auto: lanes for a call of fewer than WARMUP_AUTO_RATIO x lanes
@@ -2704,6 +2706,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.split_spin = e->split_spin;
     C.split_gthr = e->split_gthr;
     C.split_mode = e->split;
+    C.split_batch = e->split_batch;
     {
         /* live-bias warm-up (GRM_OPT_WARMUP): the first photons after a reset start as the
          * counters' history doubles, as the serial reference's bias_func sees them */
@@ -3159,6 +3162,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_SPLIT_THR: e->split_thr = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_SPLIT_SPIN: e->split_spin = v < 0 ? 0 : (v > 1 << 20 ? 1 << 20 : (int)v); return 0;
     case GRM_OPT_SPLIT_GTHR: e->split_gthr = v < 0 ? 0 : (v > 64 ? 64 : (int)v); return 0;
+    case GRM_OPT_SPLIT_BATCH: e->split_batch = v < 1 ? 1 : (v > 3 ? 3 : (int)v); return 0;
     case 18: case 20: case 21: e->err = "retired option " + std::to_string(opt); return -1;
     default: e->err = "unknown option"; return -1;
     }

@@ -340,6 +340,7 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
     bool head_done = false;
     bool warm = !karg_bad && C0.admit_n != 0;
     unsigned wait_trips = 0, spins = 0;
+    int n_round = 0; /* ready lanes of the round's first slot */
     double bias_d = bias_den(P0, C0);
     unsigned trip = 1;
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
@@ -647,11 +648,19 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
 #endif
         /* the steps ready: wait until most active lanes have one (the block then issues with nearly
          * every lane), or a few sleeps */
+        /* a round evaluates up to split_batch consecutive slots per lane: after the first, the lanes
+         * whose next slot is ready too go on at once (no loop top, refill or readiness wait between)
+         * while at least half the lanes of the round do */
+        bool spin_again = false;
+        for (int bj = 0; bj < C.split_batch; ++bj) {
         const int sc = slot_of(cons);
         const bool ready =
-            active && __hip_atomic_load(&s_tag[sc * SP_PH + p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-                          (((unsigned long long)gen << 32) | cons);
-        {
+            active && (bj == 0 || expect == E_STEP) &&
+            __hip_atomic_load(&s_tag[sc * SP_PH + p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                (((unsigned long long)gen << 32) | cons);
+        if (bj > 0) {
+            if (__popcll(__ballot(ready)) * 2 < n_round) break;
+        } else {
             const int n_ready = __popcll(__ballot(ready));
             const int n_act = __popcll(__ballot(active));
             const int need = max(1, (n_act * C.split_thr) >> 6);
@@ -662,9 +671,11 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
                 ++spins;
                 SP_T(ti[6], 1);
                 __builtin_amdgcn_s_sleep(1);
-                continue;
+                spin_again = true;
+                break; /* to the loop top (the batch loop's continue would not get there) */
             }
             spins = 0;
+            n_round = n_ready;
             SP_T(ti[1], 1);
             SP_T(ti[2], (unsigned long long)n_ready);
             SP_T(ti[3], (unsigned long long)n_act);
@@ -854,6 +865,8 @@ __device__ void sp_interaction(KArgsK *ka, const Params &P0, const Ctl &C0, int 
         ti[4] += __builtin_amdgcn_s_memtime() - tp0;
 #endif
         wave_steps += (unsigned long long)__popcll(__ballot(stepped));
+        }
+        if (spin_again) continue;
         if (warm) {
             int d = flight;
 #pragma unroll

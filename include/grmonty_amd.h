@@ -201,7 +201,9 @@ enum {
     GRM_OPT_SPLIT_SPIN = 25,
     /* split_kernel: a geometry wave makes its push attempts once this many 64ths of its live lanes
      * can (default 24), or after GRM_OPT_SPLIT_SPIN sleeps */
-    GRM_OPT_SPLIT_GTHR = 26
+    GRM_OPT_SPLIT_GTHR = 26,
+    /* split_kernel: consecutive ready slots an interaction lane evaluates per round (1..3, default 1) */
+    GRM_OPT_SPLIT_BATCH = 27
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

@@ -26,7 +26,7 @@ if grid:
 if os.environ.get("SPLIT"):
     e.set_option(G.OPT_SPLIT, int(os.environ["SPLIT"]))
     print(f"split {os.environ['SPLIT']}", flush=True)
-for key, opt in (("SPLIT_THR", 24), ("SPLIT_SPIN", 25), ("SPLIT_GTHR", 26)):
+for key, opt in (("SPLIT_THR", 24), ("SPLIT_SPIN", 25), ("SPLIT_GTHR", 26), ("SPLIT_BATCH", 27)):
     if os.environ.get(key):
         e.set_option(opt, int(os.environ[key]))
         print(f"{key} {os.environ[key]}", flush=True)
