@@ -7,7 +7,7 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 rev=$1; name=$2
 D="$R/cuda-grmonty_amd/build/rev_$name"
 rm -rf "$D"; mkdir -p "$D/csrc" "$D/include"
-for f in grm_engine.hip grm_lone.hip grm_probe.hip grm_emit.hip grm_tables.hip grm_device.h grm_emit.h; do
+for f in grm_engine.hip grm_lone.hip grm_split.hip grm_probe.hip grm_emit.hip grm_tables.hip grm_device.h grm_emit.h; do
   git -C "$R" show "$rev:cuda-grmonty_amd/csrc/$f" > "$D/csrc/$f" 2>/dev/null || rm -f "$D/csrc/$f"
 done
 git -C "$R" show "$rev:include/grmonty_amd.h" > "$D/include/grmonty_amd.h"
@@ -21,6 +21,10 @@ objs="$D/grm_engine.o"
 if [ -f "$D/csrc/grm_lone.hip" ]; then
   /opt/rocm/bin/hipcc ${FL/-mllvm -disable-machine-licm/} -mllvm -amdgpu-sched-strategy=max-ilp $VFLAGS -c "$D/csrc/grm_lone.hip" -o "$D/grm_lone.o" &
   objs="$objs $D/grm_lone.o"
+fi
+if [ -f "$D/csrc/grm_split.hip" ]; then
+  /opt/rocm/bin/hipcc $FL $VFLAGS -c "$D/csrc/grm_split.hip" -o "$D/grm_split.o" &
+  objs="$objs $D/grm_split.o"
 fi
 for f in grm_probe grm_emit grm_tables; do
   [ -f "$D/csrc/$f.hip" ] || continue
