@@ -1640,6 +1640,38 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
  * waits for them to be published and tracks them with its geometry wave.  It exits once the bulk
  * launch has ended (early_done, set by its last workgroup) and every claimed slot is done.  Without
  * it such a photon would advance one step per lane-loop trip (~7 us) until the bulk ends. */
+/* the early worker's next queue slot for the calling interaction wave, or ~0 when none will come.
+ * Out of line (it touches only global memory): the kernel's SGPR spills 344 -> 265 */
+__device__ __attribute__((noinline)) unsigned long long early_claim(const Ctl &C, unsigned long long rt_start) {
+    unsigned long long slot = 0;
+    if ((threadIdx.x & 63) == 0) slot = atomicAdd(C.early_head, 1ull);
+    slot = (unsigned long long)__builtin_amdgcn_readfirstlane((int)slot); /* < 2^31 */
+    while (true) {
+        if (slot < C.early_cap &&
+            __hip_atomic_load(C.early_ready + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == C.early_tag)
+            return slot;
+        if (__hip_atomic_load(C.early_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            /* the bulk launch has ended: every claimed hand-over is published, so a slot past the
+             * claims (or past the queue) will never come */
+            const unsigned long long tail = __hip_atomic_load(C.early_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (slot >= tail || slot >= C.early_cap) return ~0ull;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - rt_start > EARLY_ALONE_TICKS &&
+            __builtin_amdgcn_readfirstlane(
+                (int)__hip_atomic_load(C.bulk_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+            /* no bulk workgroup has started: the launches are serialised and this one runs first.
+             * Close the queue, then leave unless a bulk workgroup started meanwhile (then reopen
+             * it: a workgroup that read 1 after starting is seen here by the store-load order) */
+            if ((threadIdx.x & 63) == 0) __hip_atomic_store(C.early_live, 2ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane(
+                    (int)__hip_atomic_load(C.bulk_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+                return ~0ull;
+            if ((threadIdx.x & 63) == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __builtin_amdgcn_s_sleep(64);
+    }
+}
+
 __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ctl C) {
     const int wave = (int)(threadIdx.x >> 6);
     const int lane = (int)(threadIdx.x & 63);
@@ -1654,42 +1686,19 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
     if (wave & 1) {
-        lone_geometry(P, C, lane, pr);
+        /* one inlined copy per pair: the pair's LDS block at a constant address, as in lone_kernel
+         * (with the block indexed by the wave the geometry step compiled to ~20 more instructions and
+         * ran 1.39 us per step against the lone kernel's 1.29-1.31; now 1.32-1.37) */
+        if (wave == 1)
+            lone_geometry(P, C, lane, s_pair[0]);
+        else
+            lone_geometry(P, C, lane, s_pair[1]);
         return;
     }
     unsigned gen = 0;
     while (true) {
-        unsigned long long slot = 0;
-        if (lane == 0) slot = atomicAdd(C.early_head, 1ull);
-        slot = (unsigned long long)__builtin_amdgcn_readfirstlane((int)slot); /* < 2^31 */
-        bool got = false;
-        while (true) {
-            if (slot < C.early_cap &&
-                __hip_atomic_load(C.early_ready + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == C.early_tag) {
-                got = true;
-                break;
-            }
-            if (__hip_atomic_load(C.early_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-                /* the bulk launch has ended: every claimed hand-over is published, so a slot past the
-                 * claims (or past the queue) will never come */
-                const unsigned long long tail = __hip_atomic_load(C.early_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if (slot >= tail || slot >= C.early_cap) break;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - rt_start > EARLY_ALONE_TICKS &&
-                __builtin_amdgcn_readfirstlane(
-                    (int)__hip_atomic_load(C.bulk_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-                /* no bulk workgroup has started: the launches are serialised and this one runs first.
-                 * Close the queue, then leave unless a bulk workgroup started meanwhile (then reopen
-                 * it: a workgroup that read 1 after starting is seen here by the store-load order) */
-                if (lane == 0) __hip_atomic_store(C.early_live, 2ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_readfirstlane(
-                        (int)__hip_atomic_load(C.bulk_live, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT)) == 0)
-                    break;
-                if (lane == 0) __hip_atomic_store(C.early_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __builtin_amdgcn_s_sleep(64);
-        }
-        if (!got) break;
+        const unsigned long long slot = early_claim(C, rt_start);
+        if (slot == ~0ull) break;
         lone_interact(P, C, C.early_q[slot], lane, pr, gen);
     }
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -4,7 +4,9 @@ grandchild that lives ~634 k steps (profiles/r02u_long_photon_replay.txt, a boun
 the CPU oracle replays the same family).  Tracking that primary alone puts the grandchild on the
 serial chain of a two-wave pair; prints its steps and the pair's time per step.  With a GRM_TIMING
 build (GRMONTY_AMD_LIB=.../ab/libgrmonty_amd_timing.so) also the geometry / interaction wave split.
-Usage: python tools/long_photon_bench.py [reps]"""
+Usage: python tools/long_photon_bench.py [reps]
+EARLY=1: the chain on the early worker instead (lone hand-over off, a two-workgroup grid so that the
+worker is launched, which takes the grandchild at its 5,000th step)."""
 import os
 import struct
 import sys
@@ -25,6 +27,10 @@ e.set_option(G.OPT_BIAS_MODE, 1)
 e.set_option(G.OPT_FROZEN_SCATT, SNAP["scatt"])
 e.set_option(G.OPT_FROZEN_REC, SNAP["rec"])
 e.set_option(G.OPT_FROZEN_MAXTAU, struct.unpack("<q", struct.pack("<d", SNAP["maxtau"]))[0])
+EARLY = os.environ.get("EARLY") == "1"
+if EARLY:
+    e.set_option(G.OPT_LONE, 0)
+    e.set_option(G.OPT_GRID_BLOCKS, 2)
 for r in range(reps):
     e.reset()
     e.set_option(G.OPT_SEED, SEED)
@@ -34,9 +40,14 @@ for r in range(reps):
     e.finish()
     st = e.stats()
     inst, tm = e.debug_timing(reset=True)
-    print(f"rep {r}: longest life {st['max_photon_steps']} steps, tracked {st['n_tracked']}, lone photons "
-          f"{st['n_lone']} lone kernel {st['lone_ms']:.1f} ms, all kernels {st['last_kernel_ms']:.1f} ms -> "
-          f"{st['last_kernel_ms'] * 1e3 / max(st['max_photon_steps'], 1):.3f} us/step of the longest life", flush=True)
+    if EARLY:
+        print(f"rep {r} (early worker): longest life {st['max_photon_steps']} steps, tracked {st['n_tracked']}, early "
+              f"photons {st['n_early']}, early worker {st['early_ms']:.1f} ms, all kernels {st['last_kernel_ms']:.1f} ms -> "
+              f"{st['early_ms'] * 1e3 / max(st['max_photon_steps'], 1):.3f} us/step of the longest life", flush=True)
+    else:
+        print(f"rep {r}: longest life {st['max_photon_steps']} steps, tracked {st['n_tracked']}, lone photons "
+              f"{st['n_lone']} lone kernel {st['lone_ms']:.1f} ms, all kernels {st['last_kernel_ms']:.1f} ms -> "
+              f"{st['last_kernel_ms'] * 1e3 / max(st['max_photon_steps'], 1):.3f} us/step of the longest life", flush=True)
     if inst:
         g, i = tm[16:22], tm[36:40]
         if g[0]:
