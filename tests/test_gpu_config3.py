@@ -17,7 +17,9 @@ here every counter is u64):
     nscatt = scattered; integers below 2^53 add exactly in fp64), and every rank's kernel-side view
     of the job counters = the sums of the ranks' own counters and the max of their max tau_scatt;
   - the job's warm-up ended on every rank, within WARMUP_MS of its launch start (a job barrier that
-    never opened would hold it to the 1 s stall guard -- ADVICE r04);
+    never opened would hold it to the 1 s stall guard -- ADVICE r04), and the job admitted in
+    batches (a rank whose launch starts after the job's admission has ended -- its engine queued
+    behind the others' emission on the one GPU -- logs only the closing entry);
   - the JOB's luminosity within LUM_BAR of the photon_n = 1e6 oracle runs' mean
     (tests/golden/oracle_synth192_pn1e6.json, 6 runs, spread 0.09 %): the estimator is unbiased
     whatever the adaptive bias, and at 1.46e9 superphotons its Monte Carlo error is ~0.01 %.
@@ -64,7 +66,10 @@ def test_whole_photon_n_1e8_job_on_one_gpu(dump_dir, tmp_path):
         print(f"rank {rk}: warm-up end {ph['warmup_end_ms']} ms, {len(ph['admissions'])} admission batches, "
               f"pool drained {ph['pool_drained_ms']} ms, last exit {ph['last_exit_ms']} ms")
         assert ph["warmup_end_ms"] is not None and 0 <= ph["warmup_end_ms"] < WARMUP_MS, ph
-        assert len(ph["admissions"]) >= 2
+        # a rank that starts after the job's admission has ended (its engines queue behind the others'
+        # emission on the one GPU) sees only the closing entry
+        assert len(ph["admissions"]) >= 1
+    assert max(len(ph["admissions"]) for ph in job["per_rank_phases"]) >= 2
     o = json.load(open(os.path.join(HERE, "golden", "oracle_synth192_pn1e6.json")))["runs"]
     l_o = np.array([x["luminosity"] for x in o])
     rel = job["luminosity"] / l_o.mean() - 1
