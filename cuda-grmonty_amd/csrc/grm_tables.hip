@@ -37,16 +37,26 @@ struct TableConsts {
     double l_nu_min, d_l_nu, l_b_min, d_l_b, nfac;
 };
 
-/* klein_nishina (hotcross.cpp:144-151), the host expression with libm-grade log */
+#define GRM_CR_FN __device__ __forceinline__
+#define GRM_CR_LOG(x) log(x)
+#include "grm_crlog.h"
+
+/* klein_nishina (hotcross.cpp:144-151), the host expression, each operation rounded as the host's
+ * (no contraction) and, below w = 0.1, log(1 + 2w) correctly rounded, as glibc's is: the expression
+ * cancels ~6 digits just above w = 1e-3, where ocml's last bit of that log was ~1e-10 of sigma
+ * (grm_crlog.h); at w = 0.1 the cancellation makes a last-bit difference ~3e-14 of sigma */
 __device__ __forceinline__ double kn_sigma(double w) {
+#pragma clang fp contract(off)
     if (w < 1.0e-3) return (1.0 - 2.0 * w);
-    return (3.0 / 4.0) * (2.0 / (w * w) + (1.0 / (2.0 * w) - (1.0 + w) / (w * w * w)) * log(1.0 + 2.0 * w) +
+    const double l = w < 0.1 ? grm_cr::cr_log(1.0 + 2.0 * w) : log(1.0 + 2.0 * w);
+    return (3.0 / 4.0) * (2.0 / (w * w) + (1.0 / (2.0 * w) - (1.0 + w) / (w * w * w)) * l +
                           (1.0 + w) / ((1.0 + 2.0 * w) * (1.0 + 2.0 * w)));
 }
 
 /* grid[0..HC_N_W] = w, grid[HC_N_W+1..] = theta_e: the host's std::pow values, so that the grid
  * points (and the theta_e < HC_MIN_T switch at the first column) are the host's bit for bit */
 __global__ __launch_bounds__(TB) void hot_table_kernel(const double *grid, double *hot) {
+#pragma clang fp contract(off) /* every product and sum rounded as the host's (its build has no FMA) */
     __shared__ double s_g[HOT_NODES], s_fw[HOT_NODES], s_v[HOT_NODES];
     __shared__ int s_n;
     const int jj = blockIdx.x;
@@ -84,7 +94,7 @@ __global__ __launch_bounds__(TB) void hot_table_kernel(const double *grid, doubl
                 }
             sigma = cross * SIGMA_THOMSON;
         }
-        hot[(size_t)ii * (HC_N_T + 1) + jj] = log10(sigma);
+        hot[(size_t)ii * (HC_N_T + 1) + jj] = grm_cr::grm_log10(sigma); /* glibc's log10 construction */
     }
 }
 

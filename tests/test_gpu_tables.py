@@ -8,12 +8,17 @@ differences are ocml vs glibc last bits (exp, log, pow) and K2's two evaluations
 logarithms, so an absolute difference is the relative difference of the tabulated quantity: K2
 agrees to 1e-13 (measured ~4e-15: the device's trapezoid e^x K2(x) and std::cyl_bessel_k); nint and
 dndlnu_max, sums of 200 interpolated emissivities over a weight table that itself comes from the
-device K2, to 1e-11 (measured ~7e-13).  hotcross: most entries bit-identical; the Klein-Nishina
-expression (hotcross.cpp:144-151) cancels ~6 digits just above its w = 1e-3 switch, where a last-bit
-difference of log(1 + 2w) becomes ~1e-10 of sigma in both builds, so |d log10 sigma| <= 1e-9 (measured
-2.14e-10 at entry (111, 0), w = 1.2e-3, theta_e = 1e-4; the builder compiled without FMA contraction
-gives the same table bit for bit, profiles/r05_split/r05g_tables.log: the difference is ocml's vs
-glibc's last bits of log, which only a port of glibc's log would remove)."""
+device K2, to 1e-11 (measured ~7e-13).  hotcross: the Klein-Nishina expression (hotcross.cpp:144-151)
+cancels ~6 digits just above its w = 1e-3 switch, so a last-bit difference of its argument or of
+log(1 + 2w) becomes ~1e-10 of sigma.  The device kernel therefore rounds every product and sum as the
+host's build does (no FMA contraction: its 1 - mu v as one fma had put the argument an ulp off) and
+takes that log correctly rounded (grm_crlog.h), as glibc's is but for arguments within ~0.005 ulp of
+a rounding boundary, with the final log10 built as glibc builds it.  Measured: 2.14e-10 before (ocml
+log, contraction; the log alone left that entry unchanged), 2.75e-12 with both, 0.848 of the entries
+bit-identical (profiles/r05_tables_crlog.log); bar 3e-11, ten times that.  The table build takes
+~31-37 ms of GPU time instead of 4.4 (a double-double exp per log below w = 0.1), once per model.  What is left is glibc's misrounded logs
+(0.02 % of arguments, tests/test_crlog.py) in the cancelling range and ocml's exp in the
+Maxwell-Juttner weights."""
 import numpy as np
 import pytest
 
@@ -39,7 +44,7 @@ def test_device_tables_match_host(dump32):
         if which == 0:
             k = int(np.argmax(np.abs(d - h)))
             print(f"  worst hotcross entry (w index, theta index) {divmod(k, 81)}: host {h.flat[k]!r} device {d.flat[k]!r}")
-            assert np.max(np.abs(d[f] - h[f])) <= 1e-9 and np.mean(u == 0) > 0.5
+            assert np.max(np.abs(d[f] - h[f])) <= 3e-11 and np.mean(u == 0) > 0.8
         else:
             assert np.max(np.abs(d[f] - h[f])) <= (1e-13 if which == 1 else 1e-11), (name, np.max(np.abs(d[f] - h[f])))
     # the weight table is built on the host from the device K2: same to a few ulp
