@@ -78,9 +78,6 @@ def parse():
     ap.add_argument("--shard-of", default="",
                     help="R/N: run only rank R's zone shard of an N-rank job on this one GPU (a rehearsal of one "
                          "rank of BASELINE configs[3] -- photon_n 1e8 over 8 GPUs -- without the other ranks)")
-    ap.add_argument("--separate-emit", action="store_true",
-                    help="emit and track as two calls (grm_engine_emit + grm_engine_track_device) instead of one "
-                         "grm_engine_emit_track, whose transport launch writes the batch during its warm-up")
     ap.add_argument("--grid", type=int, default=192)
     ap.add_argument("--dump", default="", help="HARM dump to use (default: synthetic dump019-class)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
@@ -311,11 +308,8 @@ def main():
             eng.begin_pass(slot)
         eng.set_option(G.OPT_SEED, seed)
         eng.set_option(G.OPT_ID_BASE, base)
-        if args.separate_emit:
-            ptr, n_dev = eng.emit(seed=seed, z0=z0, z1=z1, stride=zst)
-            eng.track_device(ptr, n_dev)
-        else:
-            ptr, n_dev = eng.emit_track(seed=seed, z0=z0, z1=z1, stride=zst)
+        ptr, n_dev = eng.emit(seed=seed, z0=z0, z1=z1, stride=zst)
+        eng.track_device(ptr, n_dev)
         st = eng.stats()
         if slot is not None:
             eng.stash(slot)
@@ -466,10 +460,6 @@ def main():
                        # the rate of the median pass (value is the whole job's: the long-photon tail passes
                        # weigh in there)
                        "median_pass_rate": (total / args.steps) / srt[len(srt) // 2],
-                       "emission": ("grm_engine_emit + grm_engine_track_device" if args.separate_emit else
-                                    "grm_engine_emit_track: the batch written inside the transport launch by the "
-                                    "workgroups its warm-up parks; photons written there per pass: "
-                                    f"{sum(s.get('last_emit_in_launch', 0) for s in sts) // args.steps}"),
                        "transport_steps_per_s": steps_tot / (kern_ms * 1e-3), "kernel_ms_per_pass": kern_ms / args.steps,
                        "dominant_launch_ms_per_pass": big_ms / args.steps,
                        "emit_ms_per_pass": emit_ms / args.steps,

@@ -164,17 +164,6 @@ struct Ctl {
     int split_gthr; /* a geometry wave pushes once split_gthr / 64 of its live lanes can (or after split_spin sleeps) */
     int split_mode; /* 1: waves 0-3 geometry, 4-7 interaction; 2: roles by the SIMD a wave runs on */
     int split_batch; /* consecutive ready slots an interaction lane may evaluate per round */
-    /* in-launch emission (grm_engine_emit_track; emit_on = 0: the batch is already emitted): the
-     * warm-up's admission positions were emitted ahead of the launch; the workgroups parked during
-     * the warm-up emit the batch's claim positions [emit_pos0, pos_end) meanwhile, RES_CHUNK at a
-     * time (*emit_next: next position, *emit_fin: positions done), and the admission ends only once
-     * all are (no claim past the warm-up reads a photon not yet written) */
-    int emit_on;
-    EmitParams emit;
-    uint64_t emit_z0, emit_stride, emit_nz;
-    const unsigned long long *emit_off;
-    grm_init_photon *emit_out;
-    unsigned long long emit_pos0, *emit_next, *emit_fin;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -1718,28 +1707,6 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
 #endif /* GRM_LONE_TU */
 
 #if !defined(GRM_LONE_TU) && !defined(GRM_SPLIT_TU)
-/* in-launch emission by a parked wave: the next RES_CHUNK claim positions of the batch (position q is
- * photon (q mod 2^pool_sh) pool_m + q / 2^pool_sh, holes past n_pool skipped), one per lane, with the
- * emission kernel's own sampler (grm_emit.h emit_photon: the same photons, the same bits); done once
- * the positions run out */
-__device__ __forceinline__ void emit_chunk(const Params &P, const Ctl &C, int lane, bool &done) {
-    unsigned long long b = 0;
-    if (lane == 0) b = atomicAdd(C.emit_next, RES_CHUNK);
-    b = __shfl(b, 0) + C.emit_pos0;
-    if (b >= C.pos_end) {
-        done = true;
-        return;
-    }
-    const unsigned long long q = b + (unsigned long long)lane;
-    if (q < C.pos_end) {
-        const unsigned long long g = (q & ((1ull << C.pool_sh) - 1)) * C.pool_m + (q >> C.pool_sh);
-        if (g < C.n_pool)
-            emit_photon<true>(P, C.emit, C.emit_z0, C.emit_stride, C.emit_nz, C.emit_off, g, C.emit_out);
-    }
-    __threadfence(); /* the photons before the count that releases them */
-    if (lane == 0) atomicAdd(C.emit_fin, min((unsigned long long)RES_CHUNK, C.pos_end - b));
-}
-
 /* One trip of the lane state machine = at most ONE geodesic push attempt, then, if that attempt
  * completed a step, the rest of the while-loop body of track_super_photon
  * (harm_model.cpp:919-1063).  A lane that has to halve its step (push_photon's recursion,
@@ -1988,7 +1955,6 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     unsigned long long res_next = 0, res_end = 0; /* wave-uniform: reserved claim positions */
     bool head_done = false;      /* wave-uniform: the pool head has passed pos_end */
     bool warm = !karg_bad && C0.admit_n != 0; /* wave-uniform: warm-up admission in force */
-    bool emit_done = false;      /* wave-uniform: no in-launch emission work left for this wave */
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
     L.flight() = 0;
     /* wave-uniform; refreshed every trip during the warm-up and every REFRESH_TRIPS trips after it
@@ -2012,12 +1978,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         if (warm && blockIdx.x >= WARM_BLOCKS) {
             /* the warm-up's admission batches are small: the waves of the first WARM_BLOCKS
              * workgroups take them, the rest wait here without touching the counters (their polling
-             * would contend with the warm-up's own counter traffic) until the admission is over --
-             * emitting the batch meanwhile when the launch does its own emission */
-            if (C.emit_on && !emit_done) {
-                emit_chunk(P, C, lane_id, emit_done);
-                continue;
-            }
+             * would contend with the warm-up's own counter traffic) until the admission is over */
             unsigned long long end = 0;
             if (lane_id == 0) end = __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__builtin_amdgcn_readfirstlane((int)(end >> 32)) != -1 ||
@@ -2134,12 +2095,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                                         (end >= C.admit_n || (job && h >= C.admit_lim))
                                             ? ~0ull
                                             : min(C.admit_n, end + max(C.admit_b0, grow));
-                                    /* the claims past the warm-up read the batch: all of it emitted */
-                                    const bool emitted =
-                                        !C.emit_on || __hip_atomic_load(C.emit_fin, __ATOMIC_ACQUIRE,
-                                                                        __HIP_MEMORY_SCOPE_AGENT) >= C.pos_end - C.emit_pos0;
-                                    const bool opened =
-                                        (next != ~0ull || emitted) && atomicCAS(C.admit_end, end, next) == end;
+                                    const bool opened = atomicCAS(C.admit_end, end, next) == end;
                                     if (opened && next == ~0ull && job) atomicOr(C.in_flight, WARM_DONE);
                                     if (opened && C.phases) {
                                         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -2244,11 +2200,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             if (warm) {
                 /* waiting for the next batch; a barrier that never opens (it cannot, short of a
                  * counting bug) must not hang the GPU: after ~1 s give the warm-up up for all */
-                /* (not while the launch's own emission is unfinished: the claims after would read
-                 * unwritten photons; the launch watchdog still ends a stuck launch) */
-                if (++wait_trips > (1u << 21) && lane_id == 0 &&
-                    (!C.emit_on || __hip_atomic_load(C.emit_fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                                       C.pos_end - C.emit_pos0)) {
+                if (++wait_trips > (1u << 21) && lane_id == 0) {
                     __hip_atomic_store(C.admit_end, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (C.n_peers > 1) atomicOr(C.in_flight, WARM_DONE);
                 }
@@ -2705,17 +2657,8 @@ constexpr unsigned long long WARMUP_SPREAD = 4;
 
 /* one launch (+ overflow relaunches) over claim positions [pos0, pos1) of a batch of n primaries
  * interleaved as 2^sh runs of m (Ctl.pos_end) */
-/* grm_engine_emit_track: the batch (counted and allocated, not yet written) that the transport
- * launch emits itself -- or, where no warm-up parks workgroups, that is emitted just before it */
-struct EmitJob {
-    EmitParams E;
-    uint64_t z0, stride, nz;
-    const unsigned long long *off;
-    grm_init_photon *out;
-};
-
 int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, uint64_t m, uint64_t pos0,
-               uint64_t pos1, int grid, const EmitJob *ej = nullptr) {
+               uint64_t pos1, int grid) {
     if (pos1 <= pos0) return 0;
     /* overflow pool: children rarely spill (a 1,024-deep stack per wave): a few hundred per
      * photon_n = 1e6 pass, 213-238 for the 1.8e8-photon shard of BASELINE configs[3]; size
@@ -2802,30 +2745,6 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         C.admit_spread = e->warmup_spread >= 0 ? (unsigned long long)e->warmup_spread
                                                : (e->warmup == -2 && small ? 0ull : WARMUP_SPREAD);
     }
-    /* the emission of grm_engine_emit_track: inside this launch by the workgroups the warm-up parks
-     * (its admission positions first, here), else all of it ahead of the launch on the same stream */
-    if (ej) {
-        e->stats.last_emit_in_launch = 0;
-        const bool fuse = C.admit_n > 0 && pos0 == 0 && grid > (int)WARM_BLOCKS && !e->split && !C.lone_all;
-        if (fuse) {
-            if (grm_emit_positions(e->P, ej->E, ej->z0, ej->stride, ej->nz, ej->off, n, ej->out, sh, m, C.admit_n,
-                                   e->stream, e->err))
-                return -1;
-            C.emit_on = 1;
-            C.emit = ej->E;
-            C.emit_z0 = ej->z0;
-            C.emit_stride = ej->stride;
-            C.emit_nz = ej->nz;
-            C.emit_off = ej->off;
-            C.emit_out = ej->out;
-            C.emit_pos0 = C.admit_n;
-            e->stats.last_emit_in_launch = n - std::min<uint64_t>(n, C.admit_n);
-            C.emit_next = e->d_small + 14;
-            C.emit_fin = e->d_small + 15;
-        } else if (grm_emit_fill(e->P, ej->E, ej->z0, ej->stride, ej->nz, ej->off, n, ej->out, e->stream, e->err)) {
-            return -1;
-        }
-    }
     if (e->bias_mode && e->frozen_set) {
         C.f_scatt = e->fz_scatt;
         C.f_rec = e->fz_rec;
@@ -2857,8 +2776,6 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         op.clear_abort = 1;
         op.set = (1u << 0) | (1u << 1) | (1u << 2) | (1u << 7);
         op.val[0] = pass == 0 ? pos0 : 0;
-        if (pass == 0 && C.emit_on) op.set |= (1u << 14) | (1u << 15); /* in-launch emission counters */
-        if (pass > 0) C.emit_on = 0;
         if (pass == 0 && C.admit_n) {
             const unsigned long long h = C.admit_h0;
             op.set |= (1u << 4) | (1u << 5);
@@ -3020,7 +2937,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
  * index: results depend on the order only through the bias). */
 constexpr int CLAIM_SH = 12;
 
-int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n, const EmitJob *ej = nullptr) {
+int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
     if (alloc_lanes(e)) return -1;
     e->stats.last_kernel_ms = 0.0;
     e->stats.last_steps = 0;
@@ -3046,7 +2963,7 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n, const
         grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)grid, cap_wg));
     }
     e->stats.last_grid = grid;
-    if (run_passes(e, d_batch, n, sh, m, 0, n_pos, grid, ej)) return -1;
+    if (run_passes(e, d_batch, n, sh, m, 0, n_pos, grid)) return -1;
     e->id_base += n;
     return 0;
 }
@@ -3382,22 +3299,24 @@ int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_in
     return grm_engine_emit_strided(e, seed, z0, z1, 1, dev_out, n_out);
 }
 
-/* the emission's zone range and constants (consts.hpp:33-157, host libm like the host model's) */
-static int emit_prepare(grm_engine *e, uint64_t seed, int64_t &z0, int64_t &z1, int64_t stride, EmitParams &E,
-                        uint64_t &n_zones, const char *who) {
+int grm_engine_emit_strided(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, int64_t stride,
+                            grm_init_photon **dev_out, uint64_t *n_out) {
+    if (!e || !dev_out || !n_out) return -1;
     if (stride < 1) {
-        e->err = std::string(who) + ": stride < 1";
+        e->err = "grm_engine_emit_strided: stride < 1";
         return -1;
     }
     if (!e->d_ezones) {
-        e->err = std::string(who) + ": no zone table (grm_engine_emit_setup)";
+        e->err = "grm_engine_emit: no zone table (grm_engine_emit_setup)";
         return -1;
     }
     HIPCHK(e, hipSetDevice(e->device));
     if (z1 < 0 || z1 > e->n_ezones) z1 = e->n_ezones;
     if (z0 < 0) z0 = 0;
     if (z0 > z1) z0 = z1;
-    n_zones = (uint64_t)((z1 - z0 + stride - 1) / stride);
+    const uint64_t n_zones = (uint64_t)((z1 - z0 + stride - 1) / stride);
+    /* consts.hpp:33-157 emission constants, host libm like the host model's */
+    EmitParams E;
     E.zones = e->d_ezones;
     E.weight = e->d_eweight;
     E.f = e->d_ef;
@@ -3409,15 +3328,6 @@ static int emit_prepare(grm_engine *e, uint64_t seed, int64_t &z0, int64_t &z1, 
     E.jnu_d_l_k = std::log(1.0e7 / 0.002) / GRM_N_E_SAMP;
     E.k0 = (uint32_t)seed;
     E.k1 = (uint32_t)(seed >> 32);
-    return 0;
-}
-
-int grm_engine_emit_strided(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, int64_t stride,
-                            grm_init_photon **dev_out, uint64_t *n_out) {
-    if (!e || !dev_out || !n_out) return -1;
-    EmitParams E;
-    uint64_t n_zones = 0;
-    if (emit_prepare(e, seed, z0, z1, stride, E, n_zones, "grm_engine_emit")) return -1;
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     uint64_t n = 0;
     if (grm_emit_launch(e->P, E, (uint64_t)z0, (uint64_t)stride, n_zones, e->d_eoff, e->stream, &e->pin->word[4], &e->d_emit,
@@ -3431,33 +3341,6 @@ int grm_engine_emit_strided(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1
     *dev_out = e->d_emit;
     *n_out = n;
     return 0;
-}
-
-int grm_engine_emit_track(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, int64_t stride,
-                          grm_init_photon **dev_out, uint64_t *n_out) {
-    if (!e || !dev_out || !n_out) return -1;
-    EmitJob ej;
-    uint64_t n_zones = 0;
-    if (emit_prepare(e, seed, z0, z1, stride, ej.E, n_zones, "grm_engine_emit_track")) return -1;
-    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-    uint64_t n = 0;
-    if (grm_emit_count(ej.E, (uint64_t)z0, (uint64_t)stride, n_zones, e->d_eoff, e->stream, &e->pin->word[4], &e->d_emit,
-                       &e->emit_cap, &n, e->err))
-        return -1;
-    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
-    HIPCHK(e, hipEventSynchronize(e->ev1));
-    float ms = 0.f;
-    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    e->stats.last_emit_ms = ms; /* the count and scan; the photons are written inside the transport call */
-    ej.z0 = (uint64_t)z0;
-    ej.stride = (uint64_t)stride;
-    ej.nz = n_zones;
-    ej.off = e->d_eoff;
-    ej.out = e->d_emit;
-    *dev_out = e->d_emit;
-    *n_out = n;
-    if (n == 0) return 0;
-    return run_transport(e, e->d_emit, n, &ej);
 }
 
 int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm_init_photon *host_out) {

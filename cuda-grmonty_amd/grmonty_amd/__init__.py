@@ -82,8 +82,7 @@ class Stats(C.Structure):
                 ("max_launch_ms", C.c_double), ("max_launch_steps", C.c_uint64),
                 ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64), ("n_abandoned", C.c_uint64),
                 ("n_nan_photons", C.c_uint64), ("n_lone", C.c_uint64), ("lone_ms", C.c_double),
-                ("n_early", C.c_uint64), ("early_ms", C.c_double), ("last_grid", C.c_uint64),
-                ("last_emit_in_launch", C.c_uint64)]
+                ("n_early", C.c_uint64), ("early_ms", C.c_double), ("last_grid", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -126,8 +125,6 @@ SIGNATURES = {
     "grm_engine_emit": (C.c_int, [VP, C.c_uint64, C.c_int64, C.c_int64, C.POINTER(VP), C.POINTER(C.c_uint64)]),
     "grm_engine_emit_strided": (C.c_int, [VP, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.POINTER(VP),
                                           C.POINTER(C.c_uint64)]),
-    "grm_engine_emit_track": (C.c_int, [VP, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.POINTER(VP),
-                                        C.POINTER(C.c_uint64)]),
     "grm_engine_download": (C.c_int, [VP, VP, C.c_size_t, VP]),
     "grm_probe": (C.c_int, [VP, C.c_int, DP, C.c_int, DP, C.c_int, C.c_size_t]),
     "grm_engine_upload": (C.c_int, [VP, VP, C.c_size_t, C.POINTER(VP)]),
@@ -343,15 +340,6 @@ class Engine:
         p, n = VP(), C.c_uint64()
         self._check(self.L.grm_engine_emit_strided(self.h, int(seed), int(z0), int(z1), int(stride), C.byref(p),
                                                    C.byref(n)))
-        return int(p.value or 0), int(n.value)
-
-    def emit_track(self, seed: int = 123, z0: int = 0, z1: int = -1, stride: int = 1) -> tuple[int, int]:
-        """One run_simulation pass (grm_engine_emit_track): emit the superphotons of zones z0, z0 +
-        stride, ... < z1 on the GPU and track them, the emission inside the transport launch's warm-up
-        where there is one; returns (device address of the emitted batch, count) as emit() does."""
-        p, n = VP(), C.c_uint64()
-        self._check(self.L.grm_engine_emit_track(self.h, int(seed), int(z0), int(z1), int(stride), C.byref(p),
-                                                 C.byref(n)))
         return int(p.value or 0), int(n.value)
 
     def download(self, dev_ptr: int, n: int) -> np.ndarray:

@@ -122,8 +122,6 @@ typedef struct grm_stats {
     uint64_t n_early;          /* long photons handed to the concurrent early worker since the last reset */
     double early_ms;           /* the early worker's longest launch (its stream's events) since the last reset */
     uint64_t last_grid;        /* workgroups of the most recent transport call's launch (GRM_OPT_FLIGHT_RATIO) */
-    uint64_t last_emit_in_launch; /* photons the most recent grm_engine_emit_track wrote inside its transport
-                                   * launch (0: emitted ahead of it) */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
@@ -365,17 +363,6 @@ int grm_engine_emit(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, grm_in
 /* the zones z0, z0 + stride, ... < z1 (grm_model_emit_strided's set, the same photons) */
 int grm_engine_emit_strided(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, int64_t stride,
                             grm_init_photon **dev_out, uint64_t *n_out);
-/* One run_simulation pass in one call (harm_model.cpp:341-409: make_super_photon's emission, then
- * track_super_photon over the batch; the reference's CUDA build feeds cuda_super_photon::
- * track_super_photons from the emitting host threads, super_photon.cuh:55-61): the photons of
- * grm_engine_emit_strided, tracked as grm_engine_track_device would track them.  With the live
- * bias's warm-up in force the transport launch writes the batch itself -- the warm-up's admission
- * photons first, the rest by the workgroups the warm-up parks, before any claim past it -- so the
- * emission's time hides in the warm-up; otherwise the batch is emitted just before the launch.
- * *dev_out = the engine's emission buffer, which holds the whole batch afterwards (as after
- * grm_engine_emit_strided; grm_engine_download), *n_out = the batch's photon count. */
-int grm_engine_emit_track(grm_engine *e, uint64_t seed, int64_t z0, int64_t z1, int64_t stride,
-                          grm_init_photon **dev_out, uint64_t *n_out);
 /* device -> host copy of n photons from an engine buffer (tests, writers) */
 int grm_engine_download(grm_engine *e, const grm_init_photon *dev, size_t n, grm_init_photon *host_out);
 

@@ -12,10 +12,9 @@ from spectrum_stats import cell_sums_from_trace
 KEYS = ("recorded", "scattered", "steps", "luminosity")
 
 
-def run_job(eng, model, seed, shards=None, trace_cap=0, fused=False):
+def run_job(eng, model, seed, shards=None, trace_cap=0):
     """returns dict(created, recorded, scattered, steps, luminosity, spectrum, cells (if traced),
-    per_rank: list of per-rank counters); fused: each shard as one grm_engine_emit_track call (the
-    bench's pass), else emit + track_device"""
+    per_rank: list of per-rank counters)"""
     import grmonty_amd as G
     if shards is None:
         shards = [(0, -1, 1)]
@@ -30,11 +29,8 @@ def run_job(eng, model, seed, shards=None, trace_cap=0, fused=False):
         eng.set_option(G.OPT_ID_BASE, base)
         if trace_cap:
             eng.set_option(G.OPT_TRACE_CAP, trace_cap)
-        if fused:
-            p, n = eng.emit_track(seed=seed, z0=z0, z1=z1, stride=stride)
-        else:
-            p, n = eng.emit(seed=seed, z0=z0, z1=z1, stride=stride)
-            eng.track_device(p, n)
+        p, n = eng.emit(seed=seed, z0=z0, z1=z1, stride=stride)
+        eng.track_device(p, n)
         st = eng.stats()
         assert st["n_dropped"] == 0 and st["n_abandoned"] == 0
         s, n_rec, n_scatt, mt = eng.finish()

@@ -117,39 +117,3 @@ def test_emit_buffer_reused_across_passes(model64):
     assert max(counts) > min(counts)  # the count moves with the seed
     assert len(set(ptrs)) == 1
     e.close()
-
-
-def test_emit_track_writes_the_emitted_batch(dump_dir):
-    """grm_engine_emit_track at the bench's size (192^2, photon_n = 1e6, 14.5 M photons): with the
-    live bias the transport launch writes the batch itself (the warm-up's admission positions ahead of
-    it, the rest by the workgroups the warm-up parks) -- byte for byte the batch grm_engine_emit
-    writes; with a frozen bias (no warm-up) the batch is emitted ahead of the launch, the same bytes"""
-    import os
-    import grmonty_amd as G
-    from grmonty_amd.synth_dump import ensure_dump
-    path = ensure_dump(os.path.join(dump_dir, "synth192.dump"), 192, 192)
-    model = G.Model.load(path, photon_n=1_000_000).init(8, device=0)
-    e = G.Engine(model, device=0)
-    e.emit_setup(model)
-    ref_p, n = e.emit(seed=5)
-    ref = e.download(ref_p, n)
-    for frozen in (False, True):
-        e.reset()
-        e.set_option(G.OPT_SEED, 5)
-        e.set_option(G.OPT_ID_BASE, 0)
-        e.set_option(G.OPT_BIAS_MODE, 1 if frozen else 0)
-        p, n2 = e.emit_track(seed=5)
-        st = e.stats()
-        print(f"frozen={frozen}: {n2} photons, {st['last_emit_in_launch']} written inside the launch, "
-              f"{st['n_primaries']} primaries tracked, grid {st['last_grid']}")
-        assert n2 == n and st["n_dropped"] == 0 and st["n_abandoned"] == 0
-        if frozen:
-            assert st["last_emit_in_launch"] == 0
-        else:
-            assert st["last_emit_in_launch"] > 0.99 * n and st["last_grid"] > 64
-        got = e.download(p, n)
-        assert got.tobytes() == ref.tobytes()
-        e.finish()
-        assert e.stats()["n_primaries"] == n
-    e.set_option(G.OPT_BIAS_MODE, 0)
-    e.close()

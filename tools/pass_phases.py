@@ -1,8 +1,7 @@
 """Timeline of a pass's main transport launch (grm_engine_debug_phases): when the live-bias warm-up
 admission ended, when the pool's last claim chunk was taken, when the last wave left -- over a few
 bench-like passes (192^2, photon_n = 1e6, device tables).
-Usage: python tools/pass_phases.py [passes] [photon_n]   (GRM_BENCH_OPTS as in bench.py; FUSED=1: each pass
-one grm_engine_emit_track call)"""
+Usage: python tools/pass_phases.py [passes] [photon_n]   (GRM_BENCH_OPTS as in bench.py)"""
 import os
 import sys
 
@@ -23,11 +22,8 @@ for kv in filter(None, os.environ.get("GRM_BENCH_OPTS", "").split(",")):
 for s in range(n):
     e.reset()
     e.set_option(G.OPT_SEED, 123 + s)
-    if os.environ.get("FUSED") == "1":  # one grm_engine_emit_track call (the bench's pass)
-        p, cnt = e.emit_track(seed=123 + s)
-    else:
-        p, cnt = e.emit(seed=123 + s)
-        e.track_device(p, cnt)
+    p, cnt = e.emit(seed=123 + s)
+    e.track_device(p, cnt)
     st = e.stats()
     ph = e.debug_phases()
     w = e.debug_waves()
