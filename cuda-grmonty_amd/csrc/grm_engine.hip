@@ -2511,8 +2511,10 @@ struct grm_engine {
     LoneRec *d_lone = nullptr;             /* photons handed over to lone_kernel */
     unsigned long long lone_cap = 0;
     int lone = 1;                          /* GRM_OPT_LONE */
-    /* early hand-over of long photons to early_kernel on a second stream (GRM_OPT_EARLY_STEPS) */
-    int early_steps = 5000;
+    /* early hand-over of long photons to early_kernel on a second stream (GRM_OPT_EARLY_STEPS): 1,500
+     * (~100 photons a bench pass) rather than 5,000 (~1): frozen-bias replays of the tail passes end
+     * 14-48 ms sooner, the others unchanged; 1,000 fills the 1,024-slot queue */
+    int early_steps = 1500;
     bool early_serial = false; /* test: the worker ahead of the main launch on its stream */
     int karg_test = 0;         /* test: GRM_OPT_KARG_TEST */
     static constexpr unsigned long long EARLY_CAP = 1024;

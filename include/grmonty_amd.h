@@ -167,7 +167,7 @@ enum {
     GRM_OPT_LONE = 13,
     /* photons of the first warm-up admission batch (default 64; later batches double the history) */
     GRM_OPT_WARMUP_BATCH = 14,
-    /* a photon of this many steps (default 5000; 0 = off) leaves the lane loop at the top of a step
+    /* a photon of this many steps (default 1500; 0 = off) leaves the lane loop at the top of a step
      * for a two-wave pair of the early worker, which runs beside the main transport launch on a
      * second stream */
     GRM_OPT_EARLY_STEPS = 15,

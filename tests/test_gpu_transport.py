@@ -53,7 +53,7 @@ def test_photon_by_photon(setup, oracle64, lone):
     eng.set_option(G.OPT_SPLIT, 2 if lone == 7 else (1 if lone >= 5 else 0))
     eng.set_option(G.OPT_WATCHDOG_MS, 20000 if lone >= 5 else 60000)
     eng.set_option(G.OPT_LONE, 1 if lone >= 3 else lone)
-    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone in (3, 4, 6) else 5000)
+    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone in (3, 4, 6) else 1500)
     eng.set_option(G.OPT_EARLY_SERIAL, 1 if lone == 4 else 0)
     oracle64.reset()
     tr_o = oracle64.track(sel, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=snap["scatt"],
@@ -74,7 +74,7 @@ def test_photon_by_photon(setup, oracle64, lone):
     eng.set_option(G.OPT_TRACE_CAP, 0)
     eng.set_option(G.OPT_BIAS_MODE, 0)
     eng.set_option(G.OPT_LONE, 1)
-    eng.set_option(G.OPT_EARLY_STEPS, 5000)
+    eng.set_option(G.OPT_EARLY_STEPS, 1500)
     eng.set_option(G.OPT_EARLY_SERIAL, 0)
     eng.set_option(G.OPT_SPLIT, 0)
     eng.set_option(G.OPT_WATCHDOG_MS, 60000)

@@ -29,11 +29,15 @@ def main():
     ap.add_argument("--snap", default=os.path.join(REPO, "gpurun_out", "tail_snap.json"))
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--photon-n", type=float, default=1e6)
+    ap.add_argument("--opt", action="append", default=[], help="engine option K=V (grmonty_amd.OPT_*)")
     a = ap.parse_args()
     path = ensure_dump(os.path.join(REPO, "gpurun_out", "synth192.dump"), 192, 192)
     m = G.Model.load(path, photon_n=a.photon_n).init(0, device=0)
     e = G.Engine(m, 0)
     e.emit_setup(m)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        e.set_option(int(k), int(v))
     snap = json.load(open(a.snap)) if os.path.exists(a.snap) else {}
     lib = os.environ.get("GRMONTY_AMD_LIB", "in-tree")
 
@@ -63,7 +67,7 @@ def main():
         e.set_option(G.OPT_FROZEN_MAXTAU, struct.unpack("<q", struct.pack("<d", s["maxtau"]))[0])
         for r in range(a.reps):
             wall, cnt, st, c = run(seed)
-            print(json.dumps({"lib": lib, "seed": seed, "rep": r, "snapshot": s, "pass_s": round(wall, 4),
+            print(json.dumps({"lib": lib, "opts": a.opt, "seed": seed, "rep": r, "snapshot": s, "pass_s": round(wall, 4),
                               "photons": cnt, "bulk_ms": round(st["max_launch_ms"], 1),
                               "early_ms": round(st["early_ms"], 1), "n_early": st["n_early"],
                               "lone_ms": round(st["lone_ms"], 1), "n_lone": st["n_lone"],
