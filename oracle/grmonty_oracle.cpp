@@ -743,6 +743,11 @@ static Fluid fluid_zone(const grmo_model *m, int i, int j) {
 /* ------------------------------------------------------------------------- */
 static double hotcross_lkup(const grmo_model *m, double w, double theta_e) {
     ++g_dbg_hclkup;
+    /* a NaN argument (a photon whose wave vector or fluid went NaN mid-trajectory) passes every range
+     * test of hotcross.cpp:81-106 and reaches the table with (int)NaN -- undefined behaviour that
+     * indexes far outside it on x86 (INT_MIN; the reference CPU build would read there too).  The
+     * device's conversion gives 0 and its interpolant NaN; so does this */
+    if (std::isnan(w) || std::isnan(theta_e)) return std::numeric_limits<double>::quiet_NaN();
     if (w * theta_e < 1.0e-6) return SIGMA_THOMSON;
     if (theta_e < HC_MIN_T) return hc_klein_nishina(w) * SIGMA_THOMSON;
     if (w <= HC_MIN_W || w >= HC_MAX_W || theta_e <= HC_MIN_T || theta_e >= HC_MAX_T) return hotcross_num(w, theta_e);
@@ -757,6 +762,7 @@ static double hotcross_lkup(const grmo_model *m, double w, double theta_e) {
 }
 
 static double k2_eval(const grmo_model *m, double theta_e) { /* jnu_mixed.cpp:102-111, 150-158 */
+    if (std::isnan(theta_e)) return std::numeric_limits<double>::quiet_NaN(); /* as hotcross_lkup */
     if (theta_e < THETA_E_MIN) return 0.0;
     if (theta_e > JNU_MAX_T) return 2.0 * theta_e * theta_e;
     const double l_t = std::log(theta_e);
@@ -768,6 +774,7 @@ static double k2_eval(const grmo_model *m, double theta_e) { /* jnu_mixed.cpp:10
 
 static double f_eval(const grmo_model *m, double theta_e, double b_mag, double nu) { /* jnu_mixed.cpp:113-125 */
     const double k = JNU_K_FAC * nu / (b_mag * theta_e * theta_e);
+    if (std::isnan(k)) return std::numeric_limits<double>::quiet_NaN(); /* as hotcross_lkup */
     if (k > JNU_MAX_K) return 0.0;
     if (k < JNU_MIN_K) {
         const double x = std::pow(k, 1.0 / 3.0);
