@@ -14,10 +14,12 @@ Output: tests/golden/oracle_synth192_pn1e5.npz (+ .json summary).  Takes ~5 min 
     python tools/make_golden_192.py [--seeds 123,124,125,126,127,128] [--photon-n 1e5] [--merge]
 
 --merge adds the new seeds' runs to the committed fixtures (seeds already there are skipped).
+Each run is a process of its own (a run that dies is reported by seed, not waited for); --from-dir
+merges runs saved one per file by `tools/make_golden_192.py --one SEED --save-dir DIR` instead of
+running them (photon_n = 1e6 runs take ~1 h each).
 """
 import argparse
 import json
-import multiprocessing as mp
 import os
 import sys
 import time
@@ -64,6 +66,9 @@ def main():
     ap.add_argument("--out", default=OUT, help="fixture path prefix (.npz / .json)")
     ap.add_argument("--trace-cap", type=int, default=1 << 24, help="photon ends traced per run")
     ap.add_argument("--procs", type=int, default=0, help="parallel runs (default: one per seed)")
+    ap.add_argument("--one", type=int, default=None, help="run this one seed and save it (--save-dir)")
+    ap.add_argument("--save-dir", default="", help="directory of per-seed result files")
+    ap.add_argument("--from-dir", default="", help="merge the per-seed result files of this directory")
     args = ap.parse_args()
     out = args.out
     from grmonty_amd.synth_dump import ensure_dump
@@ -79,9 +84,27 @@ def main():
                             counters={k: r[k] for k in ("created", "scattered", "recorded", "steps")},
                             spectrum=g["spectrum123"] if r["seed"] == 123 else None))
         seeds = [s for s in seeds if s not in {r["seed"] for r in old}]
+    if args.one is not None:
+        r = run((path, int(args.photon_n), args.one, args.trace_cap))
+        np.savez(os.path.join(args.save_dir, f"seed{args.one}.npz"), cells=r["cells"],
+                 counters=np.array([r["counters"][k] for k in ("created", "scattered", "recorded", "steps")],
+                                   dtype=np.int64),
+                 luminosity=r["luminosity"], max_tau_scatt=r["max_tau_scatt"], wall_s=r["wall_s"])
+        print(f"seed {args.one}: {r['wall_s']:.0f} s, {r['counters']}")
+        return
     t = time.time()
-    with mp.Pool(args.procs or max(1, len(seeds))) as pool:
-        res = pool.map(run, [(path, int(args.photon_n), s, args.trace_cap) for s in seeds])
+    if args.from_dir:
+        res = []
+        for sd in seeds:
+            f = np.load(os.path.join(args.from_dir, f"seed{sd}.npz"))
+            c = f["counters"]
+            res.append(dict(seed=sd, wall_s=float(f["wall_s"]), luminosity=float(f["luminosity"]),
+                            max_tau_scatt=float(f["max_tau_scatt"]), cells=f["cells"], spectrum=None,
+                            counters=dict(zip(("created", "scattered", "recorded", "steps"), (int(x) for x in c)))))
+    else:
+        from concurrent.futures import ProcessPoolExecutor
+        with ProcessPoolExecutor(args.procs or max(1, len(seeds))) as pool:
+            res = list(pool.map(run, [(path, int(args.photon_n), s, args.trace_cap) for s in seeds]))
     print(f"{len(seeds)} oracle runs in {time.time() - t:.0f} s")
     res = old + res
     res.sort(key=lambda r: r["seed"])
