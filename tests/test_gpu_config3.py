@@ -21,7 +21,7 @@ here every counter is u64):
     batches (a rank whose launch starts after the job's admission has ended -- its engine queued
     behind the others' emission on the one GPU -- logs only the closing entry);
   - the JOB's luminosity within LUM_BAR of the photon_n = 1e6 oracle runs' mean
-    (tests/golden/oracle_synth192_pn1e6.json, 6 runs, spread 0.09 %): the estimator is unbiased
+    (tests/golden/oracle_synth192_pn1e6.json, 12 runs, spread 0.085 %): the estimator is unbiased
     whatever the adaptive bias, and at 1.46e9 superphotons its Monte Carlo error is ~0.01 %.
 """
 import json

@@ -143,7 +143,7 @@ def test_live_statistics_vs_reference_semantics(setup, model64, oracle64):
     print(f"KS D={d:.4f} crit={crit:.4f} n_eff={n1:.0f},{n2:.0f}")
     assert d < crit
     # recorded / scattered counts: over-dispersed by scattering cascades and the adaptive bias; the
-    # yardstick is the reference semantics' own seed-to-seed spread (tests/golden, 6 oracle runs)
+    # yardstick is the reference semantics' own seed-to-seed spread (tests/golden, 6-12 oracle runs)
     import json
     import os
     g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_spread_synth64.json")))
