@@ -14,7 +14,7 @@ for r in csv.DictReader(open(stats)):
     print(f"{r['Name'][:60]:60s} calls {r['Calls']:>5s} total {float(r['TotalDurationNs']) / 1e6:10.1f} ms "
           f"avg {float(r['AverageNs']) / 1e6:9.3f} ms max {float(r['MaxNs']) / 1e6:9.1f} ms")
 print("   (early_kernel runs on a second stream beside each pass's main track_kernel launch and mostly sleeps\n"
-      "    until a photon of >= 5000 steps is handed to it: its time overlaps the bulk, it is not added to it)")
+      "    until a photon of >= 1500 steps (GRM_OPT_EARLY_STEPS) is handed to it: its time overlaps the bulk, it is not added to it)")
 dur = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
              for r in csv.DictReader(open(trace)) if "track_kernel" in r["Kernel_Name"])
 b = json.loads(open(bench_json).read())
