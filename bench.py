@@ -148,15 +148,19 @@ PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def committed_traffic():
-    """(HBM bytes per dominant track_kernel launch, the PMC file's provenance) measured by rocprofv3
-    PMC passes over this same bench command (tools/traffic_summary.py -> profiles/pmc_traffic.json,
-    regenerated on the tree it describes), or (None, None)"""
+    """(HBM bytes per dominant track_kernel launch, the PMC file's provenance, whether the file was
+    measured on the kernel sources this run executes) from rocprofv3 PMC passes over this same bench
+    command (tools/traffic_summary.py -> profiles/pmc_traffic.json), or (None, None, False).  The file
+    records the content hash of the kernel sources it was measured on (grmonty_amd.srchash); only a
+    matching hash lets bench.py call traffic / this run's launch time a measured HBM rate."""
+    from grmonty_amd.srchash import kernel_source_hash
     try:
         with open(PMC_TRAFFIC) as fh:
             d = json.load(fh)
-        return d["bytes_per_dominant_launch"], d.get("source", PMC_TRAFFIC.replace(REPO + "/", ""))
+        same = d.get("kernel_src_hash") == kernel_source_hash()
+        return d["bytes_per_dominant_launch"], d.get("source", PMC_TRAFFIC.replace(REPO + "/", "")), same
     except (OSError, ValueError, KeyError):
-        return None, None
+        return None, None, False
 
 
 def pmc_traffic(path: str):
@@ -397,10 +401,14 @@ def main():
         emit_ms = sum(s["last_emit_ms"] for s in sts)
         cnt = fp64_count()
         flops_step = cnt["flops_per_step"] if cnt else None
-        traffic, traffic_src = ((pmc_traffic(args.pmc_summary), "--pmc-summary CSVs of this run") if args.pmc_summary
-                                else committed_traffic())
-        # measured HBM rate of the dominant launch: PMC bytes per launch / this run's launch time
-        hbm_gbs = traffic / (big_ms / args.steps * 1e-3) / 1e9 if traffic else None
+        traffic, traffic_src, traffic_same = ((pmc_traffic(args.pmc_summary), "--pmc-summary CSVs of this run", True)
+                                              if args.pmc_summary else committed_traffic())
+        # measured HBM rate of the dominant launch: PMC bytes per launch / this run's launch time --
+        # only when the bytes were measured on these kernels (this run's CSVs, or a committed file whose
+        # kernel-source hash matches); otherwise the traffic is reported as borrowed and no rate is formed
+        hbm_gbs = traffic / (big_ms / args.steps * 1e-3) / 1e9 if (traffic and traffic_same) else None
+        if traffic and not traffic_same:
+            traffic_src = f"BORROWED (other kernel sources): {traffic_src}"
         achieved_tf = big_steps * flops_step / (big_ms * 1e-3) / 1e12 if flops_step else None
         alg_gbs = big_steps * ALG_BYTES_PER_STEP / (big_ms * 1e-3) / 1e9
         cpu = None
@@ -441,7 +449,8 @@ def main():
                            if world > 1 else "")},
             "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": achieved_tf / FP64_PEAK_TFS if achieved_tf else None,
-                         "traffic": traffic,
+                         "traffic": traffic if traffic_same else None,
+                         "traffic_borrowed": None if traffic_same else traffic,
                          "flops_per_step": flops_step,
                          "transcendentals_per_step": cnt.get("transcendentals_per_step") if cnt else None,
                          "traffic_source": traffic_src,

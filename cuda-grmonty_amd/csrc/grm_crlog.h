@@ -82,6 +82,10 @@ GRM_CR_FN double grm_log10(double x) {
 #endif
     const double ivln10 = 4.34294481903251816668e-01, log10_2hi = 3.01029995663611771306e-01,
                  log10_2lo = 3.69423907715893078616e-13;
+    /* zero, subnormal, negative, inf and NaN arguments: the exponent rewrite below assumes a
+     * positive normal number (it would give ~-308 for 0, ~308 for inf and NaN), so these take the
+     * library log10 (NaN, -inf, inf as glibc) */
+    if (!(x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308)) return log10(x);
     uint64_t b;
     __builtin_memcpy(&b, &x, 8);
     int32_t hx = (int32_t)(b >> 32);

@@ -86,6 +86,11 @@ struct DevCounters {
 };
 static_assert(sizeof(DevCounters) == 16 * 8, "DevCounters layout (grm_engine_debug_counters)");
 constexpr unsigned long long WARM_DONE = 1ull << 63, WARM_HIST = 1ull << 32;
+/* set by the rank's transport launch as it starts (the job's start barrier, job_started) */
+constexpr unsigned long long WARM_STARTED = 1ull << 62;
+/* a rank's warm-up waits at most this long (s_memrealtime ticks, 100 MHz) for every peer's launch to
+ * start before its first claim; past it the warm-up goes on without the missing ranks */
+constexpr unsigned long long START_WAIT_TICKS = 50000000ull; /* 0.5 s */
 
 struct LoneRec;
 struct Ctl {
@@ -180,8 +185,16 @@ constexpr int LANE_XFIELDS = 10;
     X(n_scatt, 0)                                                                                    \
     X(flight, 1) /* warm-up: photons started (+) / ended (-) since the last flush */                \
     /* the lane's launch counters (widened and wave-reduced at exit) */                              \
-    X(c_tracked, 2) X(c_primaries, 3) X(c_children, 4) X(c_nstep_max, 5) X(c_long, 6)
+    X(c_tracked, 2) X(c_primaries, 3) X(c_children, 4) X(c_nstep_max, 5) X(c_long, 6)                \
+    GRM_X_TABSPEC_FIELDS(X)
+#ifdef GRM_X_TABSPEC
+/* experiment: the photon's previous hotcross cell (flat index) and K2 interval (TabSpec, grm_device.h) */
+#define GRM_X_TABSPEC_FIELDS(X) X(hc_prev, 7) X(k2_prev, 8)
+constexpr int LANE_IFIELDS = 9;
+#else
+#define GRM_X_TABSPEC_FIELDS(X)
 constexpr int LANE_IFIELDS = 7;
+#endif
 /* [field][lane], indexed with threadIdx.x so that every access is one ds_read/ds_write_b64 with an
  * immediate offset (a generic pointer here would turn them into FLAT accesses, which also count in
  * vmcnt and cost a 64-bit address register each) */
@@ -268,7 +281,7 @@ __device__ __forceinline__ void warm_job(const Ctl &C, unsigned long long &hist,
     if (lane < C.n_peers) {
         const unsigned long long v =
             __hip_atomic_load(&(C.peers[lane] + C.ctr_slot)->warm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const unsigned long long r = v & ~WARM_DONE;
+        const unsigned long long r = v & ~(WARM_DONE | WARM_STARTED);
         h = (r + (WARM_HIST >> 1)) >> 32; /* flight may be negative between a claim and its undo */
         f = (v & WARM_DONE) ? 0 : (long long)(r - h * WARM_HIST);
     }
@@ -279,6 +292,20 @@ __device__ __forceinline__ void warm_job(const Ctl &C, unsigned long long &hist,
     }
     hist = h;
     flight = f < 0 ? 0 : f;
+}
+
+/* The job's start barrier (n_peers > 1): has every rank's transport launch of this pass started
+ * (WARM_STARTED in its pass block)?  A rank that began its warm-up before the others' launches were
+ * resident -- a launch queued behind other work, or on the one-GPU emulation behind the other ranks'
+ * emission -- would admit the job's first batches alone and run its bulk on a history the job never
+ * had.  Converged callers only. */
+__device__ __forceinline__ bool job_started(const Ctl &C) {
+    const int lane = (int)(threadIdx.x & 63);
+    bool ok = true;
+    if (lane < C.n_peers)
+        ok = (__hip_atomic_load(&(C.peers[lane] + C.ctr_slot)->warm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) &
+              WARM_STARTED) != 0;
+    return __ballot(!ok) == 0;
 }
 
 /* bias_func (harm_model.cpp:1391-1404), same expression and rounding as the reference */
@@ -946,6 +973,9 @@ struct LonePair {
     LoneCtl ctl;
 };
 constexpr int LONE_PAIRS = 2; /* pairs of the concurrent worker (early_kernel: 4 waves, one per SIMD, up to 512 VGPRs) */
+/* early_kernel dispatches its geometry waves to s_pair[0] / s_pair[1] by a constant index (one inlined
+ * copy per pair): more pairs need more arms there, or a pair's interaction wave waits forever */
+static_assert(LONE_PAIRS == 2, "early_kernel's geometry dispatch assumes two pairs");
 /* early_kernel waits this long (s_memrealtime, 100 MHz) for the bulk launch to start before it
  * takes the launches for serialised and leaves */
 constexpr unsigned long long EARLY_ALONE_TICKS = 100000; /* 1 ms */
@@ -1787,6 +1817,21 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             trig_at(P, L.x, T);
             gcov_from_trig(P, T, G);
         }
+#ifdef GRM_X_TABSPEC
+        TabSpec S;
+        {
+            S.hc = L.hc_prev();
+            S.k2 = L.k2_prev();
+            S.mode = GRM_X_TABSPEC;
+            const double *ts = P.hotcross + S.hc;
+            S.t00 = ts[0];
+            S.t01 = ts[1];
+            S.t10 = ts[HC_N_T + 1];
+            S.t11 = ts[HC_N_T + 2];
+            S.k2a = P.k2[S.k2];
+            S.k2b = P.k2[S.k2 + 1];
+        }
+#endif
         zone_fetch(P, L.x, Z);
         Fluid F;
         fluid_from(P, L.x, G, Z, F);
@@ -1806,7 +1851,13 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         const bool zero = !setup && (nu < 0.0 || (!at_scatter && F.n_e == 0.0));
         double a_s = 0.0, a_a = 0.0;
         if (!zero) {
+#ifdef GRM_X_TABSPEC
+            radiation_coeffs(P, L.k, F, nu, a_s, a_a, &S);
+            L.hc_prev() = S.hc;
+            L.k2_prev() = S.k2;
+#else
             radiation_coeffs(P, L.k, F, nu, a_s, a_a);
+#endif
         }
         const double bf = (zero && !at_scatter) ? 0.0 : bias_func(bias_d, F.theta_e, L.w);
         TSTAMP(12);
@@ -1940,6 +1991,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     if (lane_id == 0) s_recn[wave] = 0;
     if (lane_id < 4) s_cnt[wave][lane_id] = 0;
     if (threadIdx.x == 0 && C0.early_q) __hip_atomic_store(C0.bulk_live, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+    /* a multi-rank warm-up: this rank's launch is resident (the job's start barrier) */
+    if (threadIdx.x == 0 && C0.n_peers > 1 && C0.admit_n != 0) atomicOr(C0.in_flight, WARM_STARTED);
     __syncthreads();
     Cold *cold = C0.cold + gtid;
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
@@ -1955,6 +2008,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     unsigned long long res_next = 0, res_end = 0; /* wave-uniform: reserved claim positions */
     bool head_done = false;      /* wave-uniform: the pool head has passed pos_end */
     bool warm = !karg_bad && C0.admit_n != 0; /* wave-uniform: warm-up admission in force */
+    /* wave-uniform: every rank of the job has started this pass (or the wait gave up); one GPU: true */
+    bool started_all = !(C0.n_peers > 1 && C0.admit_n != 0);
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
     L.flight() = 0;
     /* wave-uniform; refreshed every trip during the warm-up and every REFRESH_TRIPS trips after it
@@ -1965,6 +2020,10 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     /* per-lane launch counters, 32-bit in the loop (a lane makes < 2^32 steps per launch), widened
      * for the wave reduction at exit */
     L.c_tracked() = L.c_primaries() = L.c_children() = 0;
+#ifdef GRM_X_TABSPEC
+    L.hc_prev() = 0;
+    L.k2_prev() = 0;
+#endif
     unsigned long long wave_steps = 0; /* wave-uniform: transport steps the wave's lanes completed */
     L.c_nstep_max() = L.c_long() = 0; /* longest photon life; lives > 100k steps */
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));
@@ -2056,12 +2115,16 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                         unsigned long long j_hist = 0;
                         long long j_flight = 0;
                         if (job) warm_job(C, j_hist, j_flight);
+                        if (!started_all)
+                            started_all = job_started(C) || __builtin_amdgcn_s_memrealtime() - rt_start > START_WAIT_TICKS;
                         const unsigned long long unit = job ? WARM_HIST + 1 : 1; /* admitted + in flight */
                         if (lane_id == 0) {
                             const unsigned long long end =
                                 __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             if (end == ~0ull) {
                                 off = 1;
+                            } else if (!started_all) {
+                                /* the job's start barrier: no claim until every rank's launch runs */
                             } else {
                                 const unsigned long long head =
                                     __hip_atomic_load(C.pool_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2443,9 +2506,12 @@ __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
  * -disable-machine-licm, see there); Params and Ctl cross as bytes */
 extern "C" hipError_t grm_lone_launch(int which, unsigned grid, hipStream_t s, const void *P, size_t p_size,
                                       const void *C, size_t c_size);
-/* split_kernel lives in grm_split.hip (the bulk transport with geometry and interaction waves) */
+#ifdef GRM_WITH_SPLIT
+/* split_kernel lives in grm_split.hip (the bulk transport with geometry and interaction waves): an
+ * experiment that lost, built only into variant libraries (tools/build_variant.sh) */
 extern "C" hipError_t grm_split_launch(unsigned grid, hipStream_t s, const void *P, size_t p_size, const void *C,
                                        size_t c_size);
+#endif
 
 /* ========================================================================= */
 /* engine object + C ABI                                                      */
@@ -2515,6 +2581,18 @@ struct grm_engine {
      * (~100 photons a bench pass) rather than 5,000 (~1): frozen-bias replays of the tail passes end
      * 14-48 ms sooner, the others unchanged; 1,000 fills the 1,024-slot queue */
     int early_steps = 1500;
+    /* The queue has EARLY_CAP slots, claimed once per launch.  The photons reaching S steps fall off
+     * steeply with S (per 14.5 M-photon bench pass: ~680 at 1,200 steps, ~110 at 1,500, ~10 at
+     * 2,000, ~1 at 5,000 -- about S^-8.5), so a call of many more photons (a configs[3] shard, 1.8e8
+     * in one call) would fill the queue at 1,500 and keep its later long photons in the lane loop.
+     * The threshold therefore grows with the call past 16 M photons as (n / 16 M)^(1/8.5): the same
+     * expected hand-overs per call (~100-150) as a bench pass, 1,500 -> ~2,000 for a 1.8e8 shard. */
+    static int early_steps_for(int base, size_t n) {
+        const double ref = 16.0e6;
+        if (base <= 0 || (double)n <= ref) return base;
+        const double s = (double)base * std::pow((double)n / ref, 1.0 / 8.5);
+        return s > (double)(1 << 30) ? (1 << 30) : (int)s;
+    }
     bool early_serial = false; /* test: the worker ahead of the main launch on its stream */
     int karg_test = 0;         /* test: GRM_OPT_KARG_TEST */
     static constexpr unsigned long long EARLY_CAP = 1024;
@@ -2805,7 +2883,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.wg_exit = e->d_small + 11;
             C.early_live = e->d_small + 12;
             C.bulk_live = e->d_small + 13;
-            C.early_steps = e->early_steps;
+            C.early_steps = grm_engine::early_steps_for(e->early_steps, n);
         } else {
             C.early_q = nullptr;
         }
@@ -2843,9 +2921,12 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
          * round-robin, so with the worker's XCD full one bulk workgroup waits and starts (to find
          * the pool empty) as the bulk drains -- 255 run either way, and a full grid needs no guess
          * which XCD the worker lands on */
+#ifdef GRM_WITH_SPLIT
         if (e->split) {
             HIPCHK(e, grm_split_launch((unsigned)grid, e->stream, &e->P, sizeof(Params), &C, sizeof(Ctl)));
-        } else {
+        } else
+#endif
+        {
             hipLaunchKernelGGL(track_kernel, dim3(grid), dim3(BLOCK), 0, e->stream, e->P, C);
             HIPCHK(e, hipGetLastError());
         }
@@ -3169,11 +3250,21 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
+#ifdef GRM_WITH_SPLIT
     case GRM_OPT_SPLIT: e->split = v < 0 ? 0 : (v > 2 ? 2 : (int)v); return 0;
     case GRM_OPT_SPLIT_THR: e->split_thr = v < 1 ? 1 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_SPLIT_SPIN: e->split_spin = v < 0 ? 0 : (v > 1 << 20 ? 1 << 20 : (int)v); return 0;
     case GRM_OPT_SPLIT_GTHR: e->split_gthr = v < 0 ? 0 : (v > 64 ? 64 : (int)v); return 0;
     case GRM_OPT_SPLIT_BATCH: e->split_batch = v < 1 ? 1 : (v > 3 ? 3 : (int)v); return 0;
+#else
+    case GRM_OPT_SPLIT:
+        if (v == 0) return 0; /* track_kernel: the only bulk kernel of this build */
+        e->err = "split_kernel is not in this library (a variant build: VFLAGS=-DGRM_WITH_SPLIT tools/build_variant.sh)";
+        return -1;
+    case GRM_OPT_SPLIT_THR: case GRM_OPT_SPLIT_SPIN: case GRM_OPT_SPLIT_GTHR: case GRM_OPT_SPLIT_BATCH:
+        e->err = "split_kernel options need a variant build with -DGRM_WITH_SPLIT";
+        return -1;
+#endif
     case 18: case 20: case 21: e->err = "retired option " + std::to_string(opt); return -1;
     default: e->err = "unknown option"; return -1;
     }

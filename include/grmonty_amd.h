@@ -191,19 +191,9 @@ enum {
      * against the reference with 131 k lanes in flight, +2.3 % with 22.5 k (ratio 64), +1.0 % with
      * 16 k.  A bench pass (photon_n = 1e6, 14.5 M photons) keeps the full grid, and so do the later
      * batches of a pass fed in chunks; a frozen bias (GRM_OPT_BIAS_MODE = 1) always does. */
-    GRM_OPT_FLIGHT_RATIO = 22,
-    /* the bulk transport kernel: 0 = track_kernel (every lane its photon's whole loop body), 1 =
-     * split_kernel (geometry waves push, interaction waves evaluate) */
-    GRM_OPT_SPLIT = 23,
-    /* split_kernel: an interaction wave evaluates its ready steps once this many 64ths of its active
-     * lanes have one (default 48), or after GRM_OPT_SPLIT_SPIN short sleeps (default 4) */
-    GRM_OPT_SPLIT_THR = 24,
-    GRM_OPT_SPLIT_SPIN = 25,
-    /* split_kernel: a geometry wave makes its push attempts once this many 64ths of its live lanes
-     * can (default 24), or after GRM_OPT_SPLIT_SPIN sleeps */
-    GRM_OPT_SPLIT_GTHR = 26,
-    /* split_kernel: consecutive ready slots an interaction lane evaluates per round (1..3, default 1) */
-    GRM_OPT_SPLIT_BATCH = 27
+    GRM_OPT_FLIGHT_RATIO = 22
+    /* 23-27: the role-split bulk kernel's switches, in include/grmonty_amd_debug.h; only a variant build
+     * (tools/build_variant.sh with -DGRM_WITH_SPLIT) accepts them */
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

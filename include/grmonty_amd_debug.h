@@ -43,6 +43,24 @@ int grm_engine_debug_phases(grm_engine *e, uint64_t out[4]);
  * i + 1 opened, out[2i + 1] = photons in flight then (i < cap); returns the number of openings */
 int64_t grm_engine_debug_admissions(grm_engine *e, uint64_t *out, size_t cap);
 
+/* --- experiment: the role-split bulk kernel (csrc/grm_split.hip) ---------- */
+/* Measured 12 % slower than track_kernel and not in the product library: only a variant build
+ * (VFLAGS=-DGRM_WITH_SPLIT tools/build_variant.sh split) accepts these options; the product's
+ * grm_engine_set_option rejects them. */
+enum {
+    /* the bulk transport kernel: 0 = track_kernel, 1 = split_kernel (waves 0-3 geometry, 4-7
+     * interaction), 2 = split_kernel with the roles dealt by SIMD */
+    GRM_OPT_SPLIT = 23,
+    /* an interaction wave evaluates its ready steps once this many 64ths of its active lanes have
+     * one (default 48), or after GRM_OPT_SPLIT_SPIN short sleeps (default 4) */
+    GRM_OPT_SPLIT_THR = 24,
+    GRM_OPT_SPLIT_SPIN = 25,
+    /* a geometry wave makes its push attempts once this many 64ths of its live lanes can (default 24) */
+    GRM_OPT_SPLIT_GTHR = 26,
+    /* consecutive ready slots an interaction lane evaluates per round (1..3, default 1) */
+    GRM_OPT_SPLIT_BATCH = 27
+};
+
 /* --- per-function device probes (parity tests; one lane per input) --------------------- */
 /* which: see GRM_PROBE_* in DESIGN.md / csrc/grm_probe.hip. in/out are host arrays of
  * n * in_stride / n * out_stride doubles. */

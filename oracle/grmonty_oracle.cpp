@@ -741,8 +741,84 @@ static Fluid fluid_zone(const grmo_model *m, int i, int j) {
 /* ------------------------------------------------------------------------- */
 /* radiation.cpp:59-146, hotcross.cpp:81-106, jnu_mixed.cpp:75-158            */
 /* ------------------------------------------------------------------------- */
+#ifdef GRMO_IDXSTAT
+/* Table-index reuse statistics (tools/table_reuse.py, verdict r05 item 1a): for every hotcross / K2
+ * lookup inside a photon's transport, is its table cell the one of that photon's previous lookup?
+ * A lookup that takes no table path (Thomson, Klein-Nishina, numerical, out of range) leaves the
+ * photon with no previous cell.  g_is words: see grmo_idxstat. */
+struct IdxPrev {
+    int hi = -1, hj = -1, ki = -1;
+};
+static thread_local IdxPrev *g_ip = nullptr;
+static uint64_t g_is[16];
+static void idx_hc(int i, int j) {
+    if (!g_ip) return;
+    ++g_is[0];
+    if (g_ip->hi >= 0) {
+        ++g_is[1];
+        const int di = std::abs(i - g_ip->hi), dj = std::abs(j - g_ip->hj);
+        if (di == 0 && dj == 0) ++g_is[2];
+        if (di <= 1 && dj <= 1) ++g_is[3];
+        if (di == 0) ++g_is[4];
+        if (dj == 0) ++g_is[5];
+        if (di <= 1 && dj == 0) ++g_is[6];
+    }
+    g_ip->hi = i;
+    g_ip->hj = j;
+}
+static void idx_hc_none() { /* a lookup off the table: no previous cell for the next one */
+    if (!g_ip) return;
+    g_ip->hi = g_ip->hj = -1;
+}
+static void idx_hc_call() {
+    if (g_ip) ++g_is[7];
+}
+static void idx_k2(int i) {
+    if (!g_ip) return;
+    ++g_is[8];
+    if (g_ip->ki >= 0) {
+        ++g_is[9];
+        if (i == g_ip->ki) ++g_is[10];
+        if (std::abs(i - g_ip->ki) <= 1) ++g_is[11];
+    }
+    g_ip->ki = i;
+}
+static void idx_k2_none() {
+    if (!g_ip) return;
+    g_ip->ki = -1;
+}
+static void idx_k2_call() {
+    if (g_ip) ++g_is[12];
+}
+struct IdxScope { /* one per track_super_photon frame: a child has its own history */
+    IdxPrev mine;
+    IdxPrev *saved;
+    IdxScope() : saved(g_ip) { g_ip = &mine; }
+    ~IdxScope() { g_ip = saved; }
+};
+#define IDX_HC(i, j) idx_hc(i, j)
+#define IDX_HC_NONE() idx_hc_none()
+#define IDX_HC_CALL() idx_hc_call()
+#define IDX_K2(i) idx_k2(i)
+#define IDX_K2_NONE() idx_k2_none()
+#define IDX_K2_CALL() idx_k2_call()
+#define IDX_SCOPE() IdxScope idx_scope_
+#else
+#define IDX_HC(i, j) ((void)0)
+#define IDX_HC_NONE() ((void)0)
+#define IDX_HC_CALL() ((void)0)
+#define IDX_K2(i) ((void)0)
+#define IDX_K2_NONE() ((void)0)
+#define IDX_K2_CALL() ((void)0)
+#define IDX_SCOPE() ((void)0)
+#endif
+
 static double hotcross_lkup(const grmo_model *m, double w, double theta_e) {
     ++g_dbg_hclkup;
+    IDX_HC_CALL();
+    const bool on_table = !(std::isnan(w) || std::isnan(theta_e) || w * theta_e < 1.0e-6 || theta_e < HC_MIN_T ||
+                            w <= HC_MIN_W || w >= HC_MAX_W || theta_e <= HC_MIN_T || theta_e >= HC_MAX_T);
+    if (!on_table) IDX_HC_NONE();
     /* a NaN argument (a photon whose wave vector or fluid went NaN mid-trajectory) passes every range
      * test of hotcross.cpp:81-106 and reaches the table with (int)NaN -- undefined behaviour that
      * indexes far outside it on x86 (INT_MIN; the reference CPU build would read there too).  The
@@ -754,6 +830,7 @@ static double hotcross_lkup(const grmo_model *m, double w, double theta_e) {
     const double l_w = std::log10(w), l_t = std::log10(theta_e);
     const int i = (int)((l_w - D.hc_l_min_w) / D.hc_d_l_w);
     const int j = (int)((l_t - D.hc_l_min_t) / D.hc_d_l_t);
+    IDX_HC(i, j);
     const double d_i = (l_w - D.hc_l_min_w) / D.hc_d_l_w - i;
     const double d_j = (l_t - D.hc_l_min_t) / D.hc_d_l_t - j;
     const double lc = (1.0 - d_i) * (1.0 - d_j) * m->HC(i, j) + d_i * (1.0 - d_j) * m->HC(i + 1, j) +
@@ -762,12 +839,15 @@ static double hotcross_lkup(const grmo_model *m, double w, double theta_e) {
 }
 
 static double k2_eval(const grmo_model *m, double theta_e) { /* jnu_mixed.cpp:102-111, 150-158 */
+    IDX_K2_CALL();
+    if (std::isnan(theta_e) || theta_e < THETA_E_MIN || theta_e > JNU_MAX_T) IDX_K2_NONE();
     if (std::isnan(theta_e)) return std::numeric_limits<double>::quiet_NaN(); /* as hotcross_lkup */
     if (theta_e < THETA_E_MIN) return 0.0;
     if (theta_e > JNU_MAX_T) return 2.0 * theta_e * theta_e;
     const double l_t = std::log(theta_e);
     double d_i = (l_t - D.jnu_l_min_t) / D.jnu_d_l_t;
     const int i = (int)d_i;
+    IDX_K2(i);
     d_i -= i;
     return std::exp((1.0 - d_i) * m->k2[i] + d_i * m->k2[i + 1]);
 }
@@ -1234,6 +1314,7 @@ struct TrackCtx {
 
 static void track_super_photon(TrackCtx &C, Photon &ph, Rng &rng) { /* :894-1069 */
     grmo_model *m = C.m;
+    IDX_SCOPE();
     if (std::isnan(ph.x[0]) || std::isnan(ph.x[1]) || std::isnan(ph.x[2]) || std::isnan(ph.x[3]) ||
         std::isnan(ph.k[0]) || std::isnan(ph.k[1]) || std::isnan(ph.k[2]) || std::isnan(ph.k[3]) || ph.w == 0.0) {
         emit_trace(m, ph, 0, 4, -1, -1);
@@ -1624,6 +1705,17 @@ void grmo_model_set_max_tau_scatt(grmo_model *m, double v) { m->max_tau_scatt = 
 const double *grmo_model_field(const grmo_model *m, int which) { return m->fld[which].data(); }
 
 /* harm_model.cpp:242-266 */
+#ifdef GRMO_IDXSTAT
+/* out[0] hotcross table lookups, [1] of them with a previous table cell, [2] the same cell, [3] within
+ * +-1 in both indices, [4] same w row, [5] same theta column, [6] w +-1 and same theta, [7] hotcross
+ * lookups on any path; [8] K2 table lookups, [9] with a previous interval, [10] the same, [11] +-1,
+ * [12] K2 lookups on any path.  reset != 0 zeroes them after reading. */
+void grmo_idxstat(uint64_t out[16], int reset) {
+    for (int i = 0; i < 16; ++i) out[i] = g_is[i];
+    if (reset) std::memset(g_is, 0, sizeof(g_is));
+}
+#endif
+
 void grmo_init_geometry(grmo_model *m) {
     const size_t nz = (size_t)m->n1() * m->n2();
     m->gcov_z.assign(nz * 16, 0.0);

@@ -5,7 +5,9 @@ Each emulated rank is an engine with 1/N of the CUs (GRM_OPT_GRID_BLOCKS), the z
 gives rank r (grmonty_amd.zone_shards: every N-th zone from r), its global photon id base, and its
 own counter block per pass; with --shared the blocks are linked (grm_engine_link_peers), so every
 rank's adaptive bias runs on the job's counters as on N GPUs with grm_engine_set_peers.  The N
-passes of a seed start together from N host threads; the job's results are the ranks' sums.
+passes of a seed start together from N host threads (each rank's emission, a barrier, then the
+transport launches, which also wait for each other at the job's device-side start barrier); the job's
+results are the ranks' sums.
 
     python tests/multirank_emu.py DUMP WORLD SEEDS OUT.json [--shared] [--photon-n 1e5]
 """
@@ -65,8 +67,12 @@ def main():
                 e.set_option(G.OPT_SEED, seed)
                 e.set_option(G.OPT_ID_BASE, int(sum(counts[:r])))
                 a, b, st = shards[r]
-                go.wait()
+                # every rank's emission first, then the transport launches together: on one GPU a
+                # rank's emission queued behind the others' transport launches started its warm-up
+                # after the job's had ended (8 ranks, photon_n = 1e8: two ranks, round 5).  The
+                # launches also meet at the job's device-side start barrier (job_started).
                 p, n = e.emit(seed=seed, z0=a, z1=b, stride=st)
+                go.wait()
                 e.track_device(p, n)
                 stt = e.stats()
                 if stt["n_dropped"] or stt["n_abandoned"]:
@@ -74,6 +80,7 @@ def main():
                 spec, nr, ns, mt = e.finish()
                 out[r] = dict(spec=spec, created=n, recorded=nr, scattered=ns, steps=stt["n_steps"], max_tau=mt,
                               rec_spec=float(spec["nph"].sum()), scatt_spec=float(spec["nscatt"].sum()),
+                              n_early=stt["n_early"],
                               phases=e.debug_phases() if args.phases else None)
             except Exception as ex:  # reported below
                 err.append(repr(ex))
@@ -108,6 +115,7 @@ def main():
         job["per_rank_recorded"] = [o["recorded"] for o in out]
         job["per_rank_created"] = [o["created"] for o in out]
         job["per_rank_scattered"] = [o["scattered"] for o in out]
+        job["per_rank_n_early"] = [o["n_early"] for o in out]
         if args.phases:
             job["per_rank_phases"] = [o["phases"] for o in out]
         # the spectrum's own sums (independent of the counter blocks)

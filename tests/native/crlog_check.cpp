@@ -31,6 +31,16 @@ int main() {
         }
         if (b != std::log10(x)) ++bad_l10;
     }
-    std::printf("n %ld log_diff %ld log10_diff %ld\n", n, bad_log, bad_l10);
+    /* special arguments: zero, subnormal, negative, infinities, NaN -- grm_log10 as glibc's log10 */
+    long bad_special = 0;
+    const double sp[] = {0.0, -0.0, 4.9e-324, 1.0e-310, -1.0, -INFINITY, INFINITY, NAN};
+    for (double x : sp) {
+        const double a = grm_cr::grm_log10(x), b = std::log10(x);
+        if (!(a == b || (std::isnan(a) && std::isnan(b)))) {
+            ++bad_special;
+            std::printf("special %a %a %a\n", x, a, b);
+        }
+    }
+    std::printf("n %ld log_diff %ld log10_diff %ld special_bad %ld\n", n, bad_log, bad_l10, bad_special);
     return 0;
 }

@@ -35,8 +35,24 @@ def test_pmc_traffic_from_counter_csvs(tmp_path):
 
 
 def test_committed_traffic_has_provenance():
+    """the committed file's bytes and provenance; it counts as measured on the running kernels only
+    when its kernel-source hash equals the hash of the sources in this tree"""
     bench = pytest.importorskip("bench")
-    traffic, src = bench.committed_traffic()
+    from grmonty_amd.srchash import kernel_source_hash
+    traffic, src, same = bench.committed_traffic()
     d = json.load(open(os.path.join(REPO, "profiles", "pmc_traffic.json")))
     assert traffic == d["bytes_per_dominant_launch"] and traffic > 0
     assert src and "tree" in src
+    assert same == (d.get("kernel_src_hash") == kernel_source_hash())
+
+
+def test_borrowed_traffic_gives_no_hbm_rate(tmp_path, monkeypatch):
+    """a traffic file measured on other kernel sources is reported as borrowed: committed_traffic
+    says so, and bench.py then forms no measured HBM rate from it"""
+    bench = pytest.importorskip("bench")
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"bytes_per_dominant_launch": 1.0e10, "source": "x (tree y)",
+                             "kernel_src_hash": "0000000000000000"}))
+    monkeypatch.setattr(bench, "PMC_TRAFFIC", str(p))
+    traffic, src, same = bench.committed_traffic()
+    assert traffic == 1.0e10 and not same

@@ -10,6 +10,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cuda-grmonty_amd"))
+from grmonty_amd.srchash import kernel_source_hash  # noqa: E402
+
 
 def per_dispatch(path, counter):
     v = {}
@@ -34,6 +37,7 @@ out = {"bytes_per_dominant_launch": (2.0 * f_kb + w_kb) * 1024.0,
        "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) -- python3 bench.py --steps %d "
                   "--warmup %d --cpu-seconds 0 --overlap 0" % (bench["steps"], bench["warmup"]),
        "source": "%s (tree %s)" % (sys.argv[4], os.environ.get("TREE_REV", "?")),
+       "kernel_src_hash": kernel_source_hash(),
        "note": "the K+W largest track_kernel dispatches = one dominant launch per pass; bytes = 2 x FETCH_SIZE + "
                "WRITE_SIZE (KB -> B); the bench line of the FETCH run: " + steps}
 json.dump(out, open(sys.argv[4], "w"), indent=1)
