@@ -2331,7 +2331,15 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         }
         bool stepped = false;
         if (active) {
+#ifdef GRM_X_PVGPR
+            /* experiment: the push's uniform parameters as VGPR copies for this trip (push_params_vgpr),
+             * instead of scalar loads from the kernarg segment at their uses */
+            Params Pv = P;
+            push_params_vgpr(Pv);
+            active = !ended && transport_trip(Pv, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked, stepped);
+#else
             active = !ended && transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked, stepped);
+#endif
             if (!active) {
                 L.c_nstep_max() = max((int)L.c_nstep_max(), L.n_step);
                 L.c_long() += L.n_step > 100000 ? 1 : 0;

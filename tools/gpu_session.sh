@@ -16,7 +16,7 @@ S=" ${STEPS:-tests smoke pmc bench prof cfg3 mix} "
 export TREE_REV=$(cat .tree_rev 2>/dev/null || echo "?")
 has() { [[ "$S" == *" $1 "* ]]; }
 if has tests; then
-timeout -k 10 1500 python -u -m pytest ${TESTS:-tests} -m gpu -v -s -x --timeout 600 --timeout-method thread > gpurun_out/${T}_pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -v -s -x --timeout 600 --timeout-method thread > gpurun_out/${T}_pytest_gpu.log 2>&1
 rc=$?; grep -E "passed|failed" gpurun_out/${T}_pytest_gpu.log | tail -1; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/${T}_pytest_gpu.log | head; exit $rc; }
 fi
 if has smoke; then

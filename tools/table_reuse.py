@@ -43,10 +43,10 @@ def main():
     tot = np.zeros(16, dtype=np.float64)
     for s in [int(x) for x in a.seeds.split(",")]:
         m.reset()
-        lum = m.run_simulation(seed=s)
+        wall = m.run_simulation(seed=s)
         L.grmo_idxstat(buf, 1)
         tot += np.array(list(buf), dtype=np.float64)
-        print(f"seed {s}: L {lum:.4f} counters {m.counters()}", flush=True)
+        print(f"seed {s}: {wall:.1f} s, counters {m.counters()}", flush=True)
     hc_prev, k2_prev = tot[1], tot[9]
     r = {
         "hc_lookups": tot[7], "hc_table_frac": tot[0] / tot[7], "hc_with_prev": hc_prev / tot[7],
