@@ -67,3 +67,30 @@ def test_lag_emulator_fixture():
         for k in ("recorded", "scattered", "steps", "luminosity"):
             diff, se, z = welch_z([r[k] for r in runs], [r[k] for r in ora])
             assert abs(z) < 4.5, (cfg, k, z)
+
+
+def test_philox_serial_matches_mt19937_reference():
+    """The counter offset settled at the reference level (verdict r05, item 2; CPU only).  The
+    emulator's serial configuration is the reference's own scheduling (one photon at a time, children
+    depth-first, counters fresh every step) on the device's streams: Philox4x32-10 per photon id,
+    53-bit (0, 1] uniforms, chi^2 as -2 ln(prod u) (+ a Box-Muller z^2 for odd dof) -- SURVEY Q4,
+    proba.cuh:227-233 -- where the reference uses mt19937 with [0, 1) uniforms and libstdc++'s
+    gamma-based chi^2 (monty_rand.cpp:19-31).  If the two constructions differed in law, the serial
+    runs would sit off the mt19937 runs; with >= 60 runs on each side every counter and the
+    luminosity agree within 3 combined standard errors (measured, 64 vs 60 runs: recorded +1.00 %
+    (0.82 SE), scattered +1.30 % (0.79), steps +0.92 % (0.76), L -0.05 % (-0.67)).  So the device's
+    +1-2 % against the mt19937 fixture is not the streams': it is the concurrency of the live bias
+    (the device-scheduled emulator reproduces it, test_lag_emulator_fixture).  Round 5's +2.68 % was
+    the first 24 runs' sample."""
+    from spectrum_stats import welch_z
+    emu = json.load(open(os.path.join(HERE, "golden", "lag_emulator_synth192_pn1e5.json")))
+    ora = json.load(open(os.path.join(HERE, "golden", "oracle_synth192_pn1e5.json")))["runs"]
+    ser = [r for r in emu["runs"] if r["config"] == "serial"]
+    assert len(ser) >= 60 and len(ora) >= 60
+    assert len({r["seed"] for r in ser}) == len(ser)
+    for k in ("recorded", "scattered", "steps", "luminosity"):
+        a, b = [r[k] for r in ser], [r[k] for r in ora]
+        diff, se, z = welch_z(a, b)
+        print(f"{k:10s} serial Philox {np.mean(a):.6g} ({len(a)} runs)  mt19937 {np.mean(b):.6g} ({len(b)} runs)  "
+              f"{diff / np.mean(b):+.2%} = {z:+.2f} SE")
+        assert abs(z) < 3.0, (k, z)
