@@ -721,6 +721,18 @@ constexpr int LDS_DOUBLES_PER_LANE = 11;
 constexpr unsigned WARM_BLOCKS = 64; /* workgroups that take the warm-up's admission batches */
 constexpr unsigned PHASE_LOG = 64;   /* words of the launch's phase log (after the per-wave record) */
 constexpr unsigned long long RES_CHUNK = 64; /* claim positions a wave reserves per pool-head atomic */
+/* The launch-control words (grm_engine::d_small: pool head, in-flight, admission end, hand-over and
+ * early-worker words) one per SMALL_STRIDE words, each in a cache line of its own: the warm-up's
+ * CAS / atomics on the pool head and the in-flight count, the parked waves' polls of the admission
+ * end and the early worker's queue words would otherwise all queue on one 128-B line */
+#ifndef GRM_SMALL_STRIDE
+#define GRM_SMALL_STRIDE 32
+#endif
+constexpr int SMALL_STRIDE = GRM_SMALL_STRIDE;
+/* waves parked during the warm-up poll the admission end once per PARK_SLEEPS x s_sleep(127) */
+#ifndef GRM_PARK_SLEEPS
+#define GRM_PARK_SLEEPS 1
+#endif
 
 __device__ __forceinline__ void save_xkdk(const Slot &s, const Lane &L) {
 #pragma unroll
@@ -2042,7 +2054,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
             if (lane_id == 0) end = __hip_atomic_load(C.admit_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__builtin_amdgcn_readfirstlane((int)(end >> 32)) != -1 ||
                 __builtin_amdgcn_readfirstlane((int)end) != -1) {
-                __builtin_amdgcn_s_sleep(127);
+#pragma unroll
+                for (int z = 0; z < GRM_PARK_SLEEPS; ++z) __builtin_amdgcn_s_sleep(127);
                 continue;
             }
             warm = false;
@@ -2331,15 +2344,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         }
         bool stepped = false;
         if (active) {
-#ifdef GRM_X_PVGPR
-            /* experiment: the push's uniform parameters as VGPR copies for this trip (push_params_vgpr),
-             * instead of scalar loads from the kernarg segment at their uses */
-            Params Pv = P;
-            push_params_vgpr(Pv);
-            active = !ended && transport_trip(Pv, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked, stepped);
-#else
             active = !ended && transport_trip(P, C, L, cold, wstack, wtop, ph2, bk, bias_d, walked, stepped);
-#endif
             if (!active) {
                 L.c_nstep_max() = max((int)L.c_nstep_max(), L.n_step);
                 L.c_long() += L.n_step > 100000 ? 1 : 0;
@@ -2496,12 +2501,12 @@ __global__ __launch_bounds__(256) void ctl_kernel(CtlOp op) {
     if (op.clear_abort) op.ctr->abort = 0;
     if (op.set_warm) op.ctr->warm = op.warm_val;
     for (int i = 0; i < 16; ++i)
-        if ((op.set >> i) & 1u) op.small[i] = op.val[i];
+        if ((op.set >> i) & 1u) op.small[i * SMALL_STRIDE] = op.val[i];
     if (op.h_ctr) {
         const unsigned long long *c = reinterpret_cast<const unsigned long long *>(op.ctr);
         unsigned long long *h = reinterpret_cast<unsigned long long *>(op.h_ctr);
         for (int i = 0; i < 16; ++i) h[i] = c[i];
-        for (int i = 0; i < 16; ++i) op.h_small[i] = op.small[i];
+        for (int i = 0; i < 16; ++i) op.h_small[i] = op.small[i * SMALL_STRIDE];
         __threadfence_system();
     }
 }
@@ -2766,7 +2771,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.pos_end = pos1;
     C.pool_m = m;
     C.pool_sh = sh;
-    C.pool_head = e->d_small + 0;
+    C.pool_head = e->d_small + (0) * SMALL_STRIDE;
     C.id_base = e->id_base;
     C.key0 = (uint32_t)e->seed;
     C.key1 = (uint32_t)(e->seed >> 32);
@@ -2781,22 +2786,22 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.ctr_slot = e->ctr_slot;
     C.trace = e->trace_cap ? e->d_trace : nullptr;
     C.trace_cap = e->trace_cap;
-    C.trace_count = e->d_small + 3;
+    C.trace_count = e->d_small + (3) * SMALL_STRIDE;
     C.timing = e->d_timing;
     C.refill_min = e->refill_min;
     C.child_min = e->child_min;
     C.lanes = (int)e->lanes;
     C.bias_frozen = e->bias_mode;
     /* a multi-rank job's flight goes to the pass block, where the other ranks' gates read it */
-    C.in_flight = C.n_peers > 1 ? &e->d_ctr->warm : e->d_small + 4;
-    C.admit_end = e->d_small + 5;
+    C.in_flight = C.n_peers > 1 ? &e->d_ctr->warm : e->d_small + (4) * SMALL_STRIDE;
+    C.admit_end = e->d_small + (5) * SMALL_STRIDE;
     C.watchdog_ticks = (unsigned long long)std::max<int64_t>(e->watchdog_ms, 0) * 100000ull; /* 100 MHz */
     C.stuck = e->d_stuck;
     C.stuck_cap = STUCK_CAP;
-    C.stuck_count = e->d_small + 6;
+    C.stuck_count = e->d_small + (6) * SMALL_STRIDE;
     C.lone = e->lone ? e->d_lone : nullptr;
     C.lone_cap = e->lone_cap;
-    C.lone_count = e->d_small + 7;
+    C.lone_count = e->d_small + (7) * SMALL_STRIDE;
     C.lone_all = e->lone == 2;
     C.karg_test = e->karg_test;
     C.split_thr = e->split_thr;
@@ -2885,18 +2890,18 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.early_ready = e->d_early_ready;
             C.early_cap = grm_engine::EARLY_CAP;
             C.early_tag = ++e->launch_seq;
-            C.early_tail = e->d_small + 8;
-            C.early_head = e->d_small + 9;
-            C.early_done = e->d_small + 10;
-            C.wg_exit = e->d_small + 11;
-            C.early_live = e->d_small + 12;
-            C.bulk_live = e->d_small + 13;
+            C.early_tail = e->d_small + (8) * SMALL_STRIDE;
+            C.early_head = e->d_small + (9) * SMALL_STRIDE;
+            C.early_done = e->d_small + (10) * SMALL_STRIDE;
+            C.wg_exit = e->d_small + (11) * SMALL_STRIDE;
+            C.early_live = e->d_small + (12) * SMALL_STRIDE;
+            C.bulk_live = e->d_small + (13) * SMALL_STRIDE;
             C.early_steps = grm_engine::early_steps_for(e->early_steps, n);
         } else {
             C.early_q = nullptr;
         }
         C.ovf = e->d_ovf[dst];
-        C.ovf_count = e->d_small + 1 + dst;
+        C.ovf_count = e->d_small + (1 + dst) * SMALL_STRIDE;
         /* the per-wave record is kept of the first launch (the bulk of a call) */
         C.waves = pass == 0 ? e->d_waves : nullptr;
         C.phases = C.waves ? e->d_waves + (size_t)(e->lanes / 64) * 4 : nullptr;
@@ -3120,9 +3125,9 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
         !hip_ok(e, hipMalloc(&e->d_k2, (GRM_N_E_SAMP + 1) * sizeof(double)), "k2") ||
         !hip_ok(e, hipMalloc(&e->d_ctr_own, sizeof(DevCounters)), "counters") ||
         !hip_ok(e, hipMalloc(&e->d_spec, sizeof(grm_spectrum_cell) * N_TH_BINS * N_E_BINS), "spectrum") ||
-        !hip_ok(e, hipMalloc(&e->d_small, 16 * sizeof(unsigned long long)), "small") ||
+        !hip_ok(e, hipMalloc(&e->d_small, 16 * SMALL_STRIDE * sizeof(unsigned long long)), "small") ||
         !hip_ok(e, hipMalloc(&e->d_stuck, STUCK_CAP * STUCK_WORDS * sizeof(double)), "stuck") ||
-        !hip_ok(e, hipMemset(e->d_small, 0, 16 * sizeof(unsigned long long)), "small"))
+        !hip_ok(e, hipMemset(e->d_small, 0, 16 * SMALL_STRIDE * sizeof(unsigned long long)), "small"))
         return fail();
     if (!hip_ok(e, hipMemcpy(e->d_zones, zones.data(), nz * 8 * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
         !hip_ok(e, hipMemcpy(e->d_hot, hotcross, nhot * sizeof(double), hipMemcpyHostToDevice), "H2D") ||
@@ -3345,7 +3350,7 @@ int64_t grm_engine_trace(grm_engine *e, grm_trace *out, size_t cap) {
     if (!e || !e->d_trace) return -1;
     hipSetDevice(e->device);
     unsigned long long cnt = 0;
-    if (hipMemcpy(&cnt, e->d_small + 3, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (hipMemcpy(&cnt, e->d_small + (3) * SMALL_STRIDE, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     const size_t avail = std::min<unsigned long long>(cnt, e->trace_cap);
     const size_t k = std::min(avail, cap);
     if (k && out && hipMemcpy(out, e->d_trace, k * sizeof(grm_trace), hipMemcpyDeviceToHost) != hipSuccess) return -1;
@@ -3523,7 +3528,7 @@ int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap) {
     if (!e || !e->d_small) return -1;
     if (hipSetDevice(e->device) != hipSuccess) return -1;
     unsigned long long cnt = 0;
-    if (hipMemcpy(&cnt, e->d_small + 6, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (hipMemcpy(&cnt, e->d_small + (6) * SMALL_STRIDE, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     const size_t n = std::min<size_t>(cnt, STUCK_CAP), k = std::min(n, cap);
     if (k && out && hipMemcpy(out, e->d_stuck, k * STUCK_WORDS * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
