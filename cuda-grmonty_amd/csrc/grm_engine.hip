@@ -718,7 +718,14 @@ __device__ __forceinline__ bool push_request(const Ctl &C, const double x[4], co
  * 2 x 11 x 8 B x 512 lanes = 88 KB (+ 40 KB of lane fields, 16 KB of lane ints): no global memory
  * traffic on the halving path. */
 constexpr int LDS_DOUBLES_PER_LANE = 11;
-constexpr unsigned WARM_BLOCKS = 64; /* workgroups that take the warm-up's admission batches */
+#ifndef GRM_WARM_BLOCKS
+#define GRM_WARM_BLOCKS 64
+#endif
+#ifndef GRM_WARM_WAVES
+#define GRM_WARM_WAVES 8
+#endif
+constexpr unsigned WARM_BLOCKS = GRM_WARM_BLOCKS; /* workgroups that take the warm-up's admission batches */
+constexpr unsigned WARM_WAVES = GRM_WARM_WAVES;   /* ... and their waves that do (waves 0-3: one per SIMD) */
 constexpr unsigned PHASE_LOG = 64;   /* words of the launch's phase log (after the per-wave record) */
 constexpr unsigned long long RES_CHUNK = 64; /* claim positions a wave reserves per pool-head atomic */
 /* The launch-control words (grm_engine::d_small: pool head, in-flight, admission end, hand-over and
@@ -2046,7 +2053,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
         const Ctl &C = karg_ctl(kt);
         ++wave_trips;
         TCOUNT(4);
-        if (warm && blockIdx.x >= WARM_BLOCKS) {
+        if (warm && (blockIdx.x >= WARM_BLOCKS || (unsigned)wave >= WARM_WAVES)) {
             /* the warm-up's admission batches are small: the waves of the first WARM_BLOCKS
              * workgroups take them, the rest wait here without touching the counters (their polling
              * would contend with the warm-up's own counter traffic) until the admission is over */
