@@ -88,9 +88,7 @@ static_assert(sizeof(DevCounters) == 16 * 8, "DevCounters layout (grm_engine_deb
 constexpr unsigned long long WARM_DONE = 1ull << 63, WARM_HIST = 1ull << 32;
 /* set by the rank's transport launch as it starts (the job's start barrier, job_started) */
 constexpr unsigned long long WARM_STARTED = 1ull << 62;
-/* a rank's warm-up waits at most this long (s_memrealtime ticks, 100 MHz) for every peer's launch to
- * start before its first claim; past it the warm-up goes on without the missing ranks */
-constexpr unsigned long long START_WAIT_TICKS = 50000000ull; /* 0.5 s */
+
 
 struct LoneRec;
 struct Ctl {
@@ -156,6 +154,9 @@ struct Ctl {
     unsigned long long *early_ready, early_cap, early_tag;
     unsigned long long *early_tail, *early_head, *early_done, *wg_exit, *early_live, *bulk_live;
     int early_steps;
+    /* a multi-rank pass's warm-up waits at most this long (s_memrealtime ticks, 100 MHz) for every
+     * peer's launch of the pass to start before its first claim (0: no wait; GRM_OPT_JOB_START_WAIT_MS) */
+    unsigned long long start_wait_ticks;
     int karg_test; /* test only (GRM_OPT_KARG_TEST): the kernel-argument check expects lanes + this */
     /* The job's bias counters across ranks: peers[r] = rank r's array of per-pass counter blocks
      * (its own included; remote ones mapped over xGMI by IPC), ctr_slot = this pass's block.  With
@@ -2028,7 +2029,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     bool head_done = false;      /* wave-uniform: the pool head has passed pos_end */
     bool warm = !karg_bad && C0.admit_n != 0; /* wave-uniform: warm-up admission in force */
     /* wave-uniform: every rank of the job has started this pass (or the wait gave up); one GPU: true */
-    bool started_all = !(C0.n_peers > 1 && C0.admit_n != 0);
+    bool started_all = !(C0.n_peers > 1 && C0.admit_n != 0 && C0.start_wait_ticks != 0);
     unsigned wait_trips = 0;     /* consecutive trips idle waiting for admission */
     L.flight() = 0;
     /* wave-uniform; refreshed every trip during the warm-up and every REFRESH_TRIPS trips after it
@@ -2136,7 +2137,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
                         long long j_flight = 0;
                         if (job) warm_job(C, j_hist, j_flight);
                         if (!started_all)
-                            started_all = job_started(C) || __builtin_amdgcn_s_memrealtime() - rt_start > START_WAIT_TICKS;
+                            started_all = job_started(C) || __builtin_amdgcn_s_memrealtime() - rt_start > C.start_wait_ticks;
                         const unsigned long long unit = job ? WARM_HIST + 1 : 1; /* admitted + in flight */
                         if (lane_id == 0) {
                             const unsigned long long end =
@@ -2601,6 +2602,11 @@ struct grm_engine {
      * (~100 photons a bench pass) rather than 5,000 (~1): frozen-bias replays of the tail passes end
      * 14-48 ms sooner, the others unchanged; 1,000 fills the 1,024-slot queue */
     int early_steps = 1500;
+    /* GRM_OPT_JOB_START_WAIT_MS: default 0.  Ranks of a real multi-GPU job run their passes back to back
+     * without a host barrier between passes (bench.py), so a rank held up by a long photon would stall
+     * every other rank's next warm-up; the one-GPU emulation of N ranks, whose launches queue behind
+     * each other, sets it (tests/multirank_emu.py) */
+    int64_t job_start_wait_ms = 0;
     /* The queue has EARLY_CAP slots, claimed once per launch.  The photons reaching S steps fall off
      * steeply with S (per 14.5 M-photon bench pass: ~680 at 1,200 steps, ~110 at 1,500, ~10 at
      * 2,000, ~1 at 5,000 -- about S^-8.5), so a call of many more photons (a configs[3] shard, 1.8e8
@@ -2803,6 +2809,7 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
     C.in_flight = C.n_peers > 1 ? &e->d_ctr->warm : e->d_small + (4) * SMALL_STRIDE;
     C.admit_end = e->d_small + (5) * SMALL_STRIDE;
     C.watchdog_ticks = (unsigned long long)std::max<int64_t>(e->watchdog_ms, 0) * 100000ull; /* 100 MHz */
+    C.start_wait_ticks = (unsigned long long)e->job_start_wait_ms * 100000ull;
     C.stuck = e->d_stuck;
     C.stuck_cap = STUCK_CAP;
     C.stuck_count = e->d_small + (6) * SMALL_STRIDE;
@@ -3255,6 +3262,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
         return 0;
     case GRM_OPT_GRID_BLOCKS: e->grid_override = (int)v; return 0;
     case GRM_OPT_FLIGHT_RATIO: e->flight_ratio = v < 0 ? 0 : v; return 0;
+    case GRM_OPT_JOB_START_WAIT_MS: e->job_start_wait_ms = v < 0 ? 0 : (v > 10000 ? 10000 : v); return 0;
     case GRM_OPT_ID_BASE: e->id_base = (uint64_t)v; return 0;
     case GRM_OPT_FROZEN_SCATT: e->fz_scatt = (double)v; e->frozen_set = true; return 0;
     case GRM_OPT_FROZEN_REC: e->fz_rec = (double)v; e->frozen_set = true; return 0;

@@ -56,6 +56,7 @@ OPT_EARLY_SERIAL = 16
 OPT_KARG_TEST = 17
 OPT_WARMUP_SPREAD = 19
 OPT_FLIGHT_RATIO = 22
+OPT_JOB_START_WAIT_MS = 28
 OPT_SPLIT, OPT_SPLIT_THR, OPT_SPLIT_SPIN, OPT_SPLIT_GTHR, OPT_SPLIT_BATCH = 23, 24, 25, 26, 27
 N_TH_BINS, N_E_BINS = 6, 200
 

@@ -191,9 +191,15 @@ enum {
      * against the reference with 131 k lanes in flight, +2.3 % with 22.5 k (ratio 64), +1.0 % with
      * 16 k.  A bench pass (photon_n = 1e6, 14.5 M photons) keeps the full grid, and so do the later
      * batches of a pass fed in chunks; a frozen bias (GRM_OPT_BIAS_MODE = 1) always does. */
-    GRM_OPT_FLIGHT_RATIO = 22
+    GRM_OPT_FLIGHT_RATIO = 22,
     /* 23-27: the role-split bulk kernel's switches, in include/grmonty_amd_debug.h; only a variant build
      * (tools/build_variant.sh with -DGRM_WITH_SPLIT) accepts them */
+    /* a multi-rank job (grm_engine_set_peers / grm_engine_link_peers): a pass's warm-up waits at most
+     * this many ms for every rank's transport launch of the pass to start before its first claim, so
+     * that no rank begins the job's warm-up alone (default 0 = no wait: ranks that run their passes
+     * back to back stay uncoupled; the one-GPU emulation of N ranks, whose launches queue behind each
+     * other, sets 500) */
+    GRM_OPT_JOB_START_WAIT_MS = 28
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */
