@@ -213,6 +213,7 @@ def main():
     # device, so the job's one reduction of the stashed passes goes over gloo instead, with the same
     # sum / max split of the engine's packing (tests/test_gpu_multirank.py reduces it the same way)
     shared_gpu = False
+    reduce_note = ""
     devs = [local]
     threads = args.threads or host_threads(world)
     # the partition: the job's ranks, and this process's place in it (--shard-of R/N: one rank of an
@@ -250,10 +251,27 @@ def main():
         devs = [None] * world
         dist.all_gather_object(devs, local)
         shared_gpu = len(set(devs)) < world
-        if not shared_gpu:
+        reduce_note = ""
+        if not shared_gpu and os.environ.get("GRM_BENCH_REDUCE", "") != "gloo":
+            # RCCL over xGMI; a rank whose communicator cannot be created makes the whole job reduce
+            # over gloo instead (the same packing and sum / max split), and the line says so
             uid = [G.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            engine.comm_init(uid[0], world, rank)
+            err = ""
+            try:
+                engine.comm_init(uid[0], world, rank)
+            except RuntimeError as ex:
+                err = repr(ex)
+            errs = [None] * world
+            dist.all_gather_object(errs, err)
+            if any(errs):
+                shared_gpu = True
+                reduce_note = f" (RCCL unavailable: {next(e for e in errs if e)[:120]}; reduced over gloo)"
+                if rank == 0:
+                    print(f"WARNING: RCCL communicator failed{reduce_note}", file=sys.stderr, flush=True)
+        elif not shared_gpu:
+            shared_gpu = True
+            reduce_note = " (GRM_BENCH_REDUCE=gloo)"
     engine.emit_setup(model)  # the zone table is resident in HBM before the timed region
     bias_counters = "single GPU"
     valid_for_parity = True
@@ -444,7 +462,8 @@ def main():
                        "valid_for_parity": valid_for_parity,
                        "peer_access": peer_matrix,
                        "parallelism": f"strided zone shards x{world}" + (
-                           (", ranks sharing GPUs (rehearsal): passes stashed on the device, one gloo reduction per job"
+                           ((", ranks sharing GPUs (rehearsal)" if len(set(devs)) < world else "") +
+                            ", passes stashed on the device, one gloo reduction per job" + reduce_note
                             if shared_gpu else ", passes stashed on the device, one RCCL all-reduce per job")
                            if world > 1 else "")},
             "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
