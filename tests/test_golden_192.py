@@ -4,9 +4,9 @@ the 192x192 dump019-class synthetic dump at photon_n = 1e5 (BASELINE configs[0])
 
 These tests calibrate the statistic the GPU parity test (tests/test_gpu_parity_192.py) applies to
 the device: independent reference-semantics runs must pass the binned Kish-N KS test on nu L_nu
-against each other, per theta bin and summed, at the test's own alpha (1e-4 per statistic); at
-alpha = 1e-3 the fraction of the (pairs x 7) statistics over the threshold must stay near 1e-3 (a
-max over hundreds of pairs at 1e-3 would fail by chance)."""
+against each other, per theta bin and summed: the fraction of the (pairs x 7) statistics over the
+test's own threshold (alpha = 1e-4) and over alpha = 1e-3 must stay near those rates (the maximum over
+thousands of pairs would exceed either by chance)."""
 import json
 import os
 
@@ -23,17 +23,21 @@ FIXTURES = [os.path.join(HERE, "golden", f"oracle_synth192_{p}") for p in ("pn1e
 def test_oracle_seeds_pass_binned_ks(G):
     g = np.load(G + ".npz")
     cells = g["cells"]
-    worst, over, tot = 0.0, 0, 0
+    worst, over, over4, tot = 0.0, 0, 0, 0
     for i in range(len(cells)):
         for j in range(i + 1, len(cells)):
             for th in [None, 0, 1, 2, 3, 4, 5]:
                 d, n1, n2 = binned_ks(cells[i], cells[j], th)
                 worst = max(worst, d / ks_crit(n1, n2, 1e-4))
+                over4 += d >= ks_crit(n1, n2, 1e-4)
                 over += d >= ks_crit(n1, n2, 1e-3)
                 tot += 1
-    print(f"{len(cells)} runs: worst D / crit(alpha=1e-4) over {tot} statistics: {worst:.2f}; over crit(1e-3): "
-          f"{over} of {tot}")
-    assert worst < 1.0
+    print(f"{len(cells)} runs: worst D / crit(alpha=1e-4) over {tot} statistics: {worst:.2f}; over crit(1e-4): "
+          f"{over4} of {tot} (nominal {1e-4 * tot:.1f}); over crit(1e-3): {over} of {tot} (nominal {1e-3 * tot:.1f})")
+    # the statistic is calibrated when independent reference runs exceed its critical values at about
+    # the nominal rates (the maximum over all pairs is not a calibration: 102 runs make 36 k statistics,
+    # ~3.6 of which exceed crit(1e-4) by chance)
+    assert over4 <= max(2, 5e-4 * tot)
     assert over <= max(2, 0.01 * tot)
 
 
@@ -77,8 +81,9 @@ def test_philox_serial_matches_mt19937_reference():
     proba.cuh:227-233 -- where the reference uses mt19937 with [0, 1) uniforms and libstdc++'s
     gamma-based chi^2 (monty_rand.cpp:19-31).  If the two constructions differed in law, the serial
     runs would sit off the mt19937 runs; with >= 60 runs on each side every counter and the
-    luminosity agree within 3 combined standard errors (measured, 64 vs 60 runs: recorded +1.00 %
-    (0.82 SE), scattered +1.30 % (0.79), steps +0.92 % (0.76), L -0.05 % (-0.67)).  So the device's
+    luminosity agree within 3 combined standard errors (measured, 64 vs 102 runs: recorded +0.85 %
+    (0.85 SE), scattered +1.14 % (0.83), steps +0.79 % (0.79), L -0.01 % (-0.10); against the first
+    60 mt19937 runs +1.00 / +1.30 / +0.92 / -0.05 %).  So the device's
     +1-2 % against the mt19937 fixture is not the streams': it is the concurrency of the live bias
     (the device-scheduled emulator reproduces it, test_lag_emulator_fixture).  Round 5's +2.68 % was
     the first 24 runs' sample."""
