@@ -956,18 +956,8 @@ __device__ __forceinline__ double alpha_inv_abs(const Params &P, double nu, doub
  * SIMD: both table indices are formed first and all six table loads (hotcross 4, K2 2) are issued
  * unconditionally (index 0 when a branch does not use the table), so their L2 latency overlaps
  * sin(theta), the synchrotron and Planck terms instead of being exposed twice in a row. */
-/* Experiment (GRM_X_TABSPEC builds, tools/build_variant.sh; never in the product): the six table values
- * loaded with the zone gather from the photon's previous table cell (hc = flat hotcross index, k2 = K2
- * interval), before the fluid that indexes them is known.  mode 1: used as they are (an upper bound on
- * what removing the table round trip can give; sigma then comes from the neighbouring cell when the
- * cell changed), mode 2: a lane whose cell changed reloads (exact). */
-struct TabSpec {
-    double t00, t01, t10, t11, k2a, k2b;
-    int hc, k2, mode;
-};
-
 __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k[4], const Fluid &F, double nu,
-                                                 double &a_s, double &a_a, TabSpec *S = nullptr) {
+                                                 double &a_s, double &a_a) {
     const double theta_e = F.theta_e, n_e = F.n_e, b = F.b;
     const double ln_te = flog(theta_e);
     /* hotcross lookup index (hotcross.cpp:82-100) */
@@ -988,33 +978,8 @@ __device__ __forceinline__ void radiation_coeffs(const Params &P, const double k
     double dk = k2_table ? udiv(ln_te - P.jnu_l_min_t, P.jnu_d_l_t, P.jnu_i_d_l_t) : 0.0;
     const int ik = k2_table ? min((int)dk, GRM_N_E_SAMP - 1) : 0;
     const double *t = P.hotcross + (size_t)i * (HC_N_T + 1) + j;
-    double t00, t01, t10, t11, k2a, k2b;
-    if (S) {
-        const int flat = i * (HC_N_T + 1) + j;
-        if (S->mode == 2 && (flat != S->hc || ik != S->k2)) {
-            S->t00 = t[0];
-            S->t01 = t[1];
-            S->t10 = t[HC_N_T + 1];
-            S->t11 = t[HC_N_T + 2];
-            S->k2a = P.k2[ik];
-            S->k2b = P.k2[ik + 1];
-        }
-        t00 = S->t00;
-        t01 = S->t01;
-        t10 = S->t10;
-        t11 = S->t11;
-        k2a = S->k2a;
-        k2b = S->k2b;
-        S->hc = hc_table ? flat : S->hc;
-        S->k2 = k2_table ? ik : S->k2;
-    } else {
-        t00 = t[0];
-        t01 = t[1];
-        t10 = t[HC_N_T + 1];
-        t11 = t[HC_N_T + 2];
-        k2a = P.k2[ik];
-        k2b = P.k2[ik + 1];
-    }
+    const double t00 = t[0], t01 = t[1], t10 = t[HC_N_T + 1], t11 = t[HC_N_T + 2];
+    const double k2a = P.k2[ik], k2b = P.k2[ik + 1];
     /* table-independent work while the loads are in flight: sin(theta) (bk_sin), the synchrotron
      * frequency terms, the Planck denominator */
     const double sin_theta = bk_sin(k, F, P.b_unit);

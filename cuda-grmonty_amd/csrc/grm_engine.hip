@@ -186,16 +186,8 @@ constexpr int LANE_XFIELDS = 10;
     X(n_scatt, 0)                                                                                    \
     X(flight, 1) /* warm-up: photons started (+) / ended (-) since the last flush */                \
     /* the lane's launch counters (widened and wave-reduced at exit) */                              \
-    X(c_tracked, 2) X(c_primaries, 3) X(c_children, 4) X(c_nstep_max, 5) X(c_long, 6)                \
-    GRM_X_TABSPEC_FIELDS(X)
-#ifdef GRM_X_TABSPEC
-/* experiment: the photon's previous hotcross cell (flat index) and K2 interval (TabSpec, grm_device.h) */
-#define GRM_X_TABSPEC_FIELDS(X) X(hc_prev, 7) X(k2_prev, 8)
-constexpr int LANE_IFIELDS = 9;
-#else
-#define GRM_X_TABSPEC_FIELDS(X)
+    X(c_tracked, 2) X(c_primaries, 3) X(c_children, 4) X(c_nstep_max, 5) X(c_long, 6)
 constexpr int LANE_IFIELDS = 7;
-#endif
 /* [field][lane], indexed with threadIdx.x so that every access is one ds_read/ds_write_b64 with an
  * immediate offset (a generic pointer here would turn them into FLAT accesses, which also count in
  * vmcnt and cost a 64-bit address register each) */
@@ -1837,21 +1829,6 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
             trig_at(P, L.x, T);
             gcov_from_trig(P, T, G);
         }
-#ifdef GRM_X_TABSPEC
-        TabSpec S;
-        {
-            S.hc = L.hc_prev();
-            S.k2 = L.k2_prev();
-            S.mode = GRM_X_TABSPEC;
-            const double *ts = P.hotcross + S.hc;
-            S.t00 = ts[0];
-            S.t01 = ts[1];
-            S.t10 = ts[HC_N_T + 1];
-            S.t11 = ts[HC_N_T + 2];
-            S.k2a = P.k2[S.k2];
-            S.k2b = P.k2[S.k2 + 1];
-        }
-#endif
         zone_fetch(P, L.x, Z);
         Fluid F;
         fluid_from(P, L.x, G, Z, F);
@@ -1871,13 +1848,7 @@ __device__ bool transport_trip(const Params &P, const Ctl &C, Lane &L, Cold *col
         const bool zero = !setup && (nu < 0.0 || (!at_scatter && F.n_e == 0.0));
         double a_s = 0.0, a_a = 0.0;
         if (!zero) {
-#ifdef GRM_X_TABSPEC
-            radiation_coeffs(P, L.k, F, nu, a_s, a_a, &S);
-            L.hc_prev() = S.hc;
-            L.k2_prev() = S.k2;
-#else
             radiation_coeffs(P, L.k, F, nu, a_s, a_a);
-#endif
         }
         const double bf = (zero && !at_scatter) ? 0.0 : bias_func(bias_d, F.theta_e, L.w);
         TSTAMP(12);
@@ -2040,10 +2011,6 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD) void track_kernel(Params
     /* per-lane launch counters, 32-bit in the loop (a lane makes < 2^32 steps per launch), widened
      * for the wave reduction at exit */
     L.c_tracked() = L.c_primaries() = L.c_children() = 0;
-#ifdef GRM_X_TABSPEC
-    L.hc_prev() = 0;
-    L.k2_prev() = 0;
-#endif
     unsigned long long wave_steps = 0; /* wave-uniform: transport steps the wave's lanes completed */
     L.c_nstep_max() = L.c_long() = 0; /* longest photon life; lives > 100k steps */
     const unsigned long long lt_mask = (lane_id == 0) ? 0ull : (~0ull >> (64 - lane_id));

@@ -33,7 +33,8 @@ int64_t grm_engine_debug_stuck(grm_engine *e, double *out, size_t cap);
  * n_overflow, n_dropped, n_primaries, max photon steps, lives > 1e5 steps, n_abandoned, abort, n_nan,
  * waves whose kernel-argument check failed, and word 15 = the multi-rank warm-up state of the
  * pass block (photons admitted << 32, plus the photons in flight as a signed low word, plus bit 63
- * once this rank's admission is over; 0 on a single GPU) */
+ * once this rank's admission is over and bit 62 once this rank's launch of the pass has started --
+ * the job's start barrier, GRM_OPT_JOB_START_WAIT_MS; 0 on a single GPU) */
 int grm_engine_debug_counters(grm_engine *e, uint64_t out[16]);
 /* diagnostic: the phases of the last call's main launch, s_memrealtime ticks (100 MHz): first wave
  * start, end of the live-bias warm-up admission (0 = none), the pool's last claim chunk taken (0 =
