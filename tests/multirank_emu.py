@@ -46,7 +46,8 @@ def main():
         e.set_option(G.OPT_GRID_BLOCKS, max(1, 256 // world))
         # the ranks' launches queue behind each other on the one GPU: the job's device-side start
         # barrier keeps every rank in the job's warm-up (on N GPUs launched together it is not needed)
-        e.set_option(G.OPT_JOB_START_WAIT_MS, 500)
+        if not args.sequential:  # ranks run one after another there: nothing to wait for
+            e.set_option(G.OPT_JOB_START_WAIT_MS, 500)
         for kv in args.opt:
             k, v = kv.split("=")
             e.set_option(int(k), int(v))
