@@ -3036,7 +3036,16 @@ int run_transport(grm_engine *e, const grm_init_photon *d_batch, size_t n) {
      * chunks on the full grid */
     int grid = e->grid;
     if (!e->bias_mode && e->flight_ratio > 0) {
-        const uint64_t cap_wg = (e->history + n) / ((uint64_t)e->flight_ratio * BLOCK);
+        /* A multi-rank job's small calls run on half those lanes: with the job's counters the ranks'
+         * concurrent launches lag the job's history more than one GPU's launch with as many lanes
+         * (emulated 8-rank jobs at photon_n = 1e5, 96 each, the same seeds: recorded +2.97 % at ratio
+         * 96, +1.42 % at 192; one GPU +1.00 / +0.92 %, the serial reference on the same streams +0.85 %;
+         * DESIGN.md §7).  Large calls (>= WARMUP_AUTO_RATIO x the full grid's lanes: the bench's 1e6
+         * per rank, a configs[3] shard) keep the ratio, so the cap does not bind there. */
+        const bool job = e->ctr_slot >= 0 && e->d_peers && e->n_peers > 1;
+        const uint64_t full = (uint64_t)e->grid * BLOCK;
+        const uint64_t ratio = (uint64_t)e->flight_ratio * ((job && e->history + n < WARMUP_AUTO_RATIO * full) ? 2 : 1);
+        const uint64_t cap_wg = (e->history + n) / (ratio * BLOCK);
         grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)grid, cap_wg));
     }
     e->stats.last_grid = grid;

@@ -190,7 +190,9 @@ enum {
      * 192^2, photon_n = 1e5 (1.45 M photons in one call, 96 seeds each): recorded +4.4 %
      * against the reference with 131 k lanes in flight, +2.3 % with 22.5 k (ratio 64), +1.0 % with
      * 16 k.  A bench pass (photon_n = 1e6, 14.5 M photons) keeps the full grid, and so do the later
-     * batches of a pass fed in chunks; a frozen bias (GRM_OPT_BIAS_MODE = 1) always does. */
+     * batches of a pass fed in chunks; a frozen bias (GRM_OPT_BIAS_MODE = 1) always does.  A
+     * multi-rank job's calls of fewer than 32 x the grid's lanes run at twice this ratio (their
+     * concurrent ranks lag the job's history more). */
     GRM_OPT_FLIGHT_RATIO = 22,
     /* 23-27: the role-split bulk kernel's switches, in include/grmonty_amd_debug.h; only a variant build
      * (tools/build_variant.sh with -DGRM_WITH_SPLIT) accepts them */
