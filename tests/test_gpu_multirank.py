@@ -11,8 +11,10 @@
    within Z_MAX combined standard errors (no allowance: the sharding faults this test exists for
    are +17 to +43 %, below, and the job's warm-up now ramps job-wide -- each rank admits 1/N of a
    single GPU's batches behind a barrier at 1/16 of the job's history, grm_engine.hip run_passes,
-   DESIGN.md §7: 8 ranks +5 % at 1/2, +1.2 to +3.7 % at 1/16); and every rank's view of the job counters (the
-   kernels' own summation path) must equal the sums of the ranks'.
+   DESIGN.md §7: 8 ranks +5 % at 1/2, +1.2 to +3.7 % at 1/16; and a multi-rank job's small calls run
+   at twice the in-flight ratio since round 6: 96-job 8-rank sessions +2.97 % at ratio 96, +1.42 % at
+   192); and every rank's view of the job counters (the kernels' own summation path) must equal the
+   sums of the ranks'.
    Without the link each rank's bias runs on its own history, N times shorter: +18 / +30 / +35 %
    recorded at 2 / 4 / 8 ranks with strided shards (profiles/r03b_pytest_multirank_unshared.log),
    +17 / +30 / +43 % with contiguous ones (profiles/r03a_multirank_contiguous.log).
