@@ -170,6 +170,12 @@ struct Ctl {
     int split_gthr; /* a geometry wave pushes once split_gthr / 64 of its live lanes can (or after split_spin sleeps) */
     int split_mode; /* 1: waves 0-3 geometry, 4-7 interaction; 2: roles by the SIMD a wave runs on */
     int split_batch; /* consecutive ready slots an interaction lane may evaluate per round */
+    /* the early worker's own children (GRM_OPT_EARLY_CHILDREN): a scattering on a pair appends the
+     * child's scatter request to the early queue (LoneRec::pad = 1, early_child_push), where the next
+     * free pair sets it up and tracks it (early_child_setup); *early_fin counts the queue slots
+     * finished -- tracked, or given up by a pair that left -- and *early_kids the children appended */
+    int early_kids_on;
+    unsigned long long *early_fin, *early_kids;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -928,6 +934,7 @@ struct alignas(16) LoneRec {
     int32_t n_step, n_scatt, pad;
 };
 static_assert(sizeof(LoneRec) == 256, "LoneRec layout");
+static_assert(sizeof(SReq) <= offsetof(LoneRec, pad), "an early-queue slot holds a scatter request below its pad word");
 
 __device__ __forceinline__ void export_lone(LoneRec *r, const Lane &L, const Cold *cold) {
     /* field by field (a LoneRec built in registers first would add 68 VGPRs at this point of the loop) */
@@ -957,6 +964,31 @@ __device__ __forceinline__ void push_overflow(const Ctl &C, const double x[4], c
                                               int n_scatt, const Cold *cold, const Fluid &F, double wc) {
     SReq R;
     make_sreq(R, x, k, rng, n_scatt, cold, F, wc);
+    push_overflow_req(C, R);
+}
+
+/* the child of an early-worker photon's scattering (lane 0): its scatter request goes into a slot of
+ * the early queue, marked as a request (LoneRec::pad = 1; the SReq fills the slot's first 192 B), and
+ * the next free pair of the worker sets it up and tracks it at once (early_child_setup), as the
+ * reference tracks a child as soon as it is made (harm_model.cpp:1016-1023); the overflow pool when
+ * the queue is full.  A slot claimed past the cap is never published, as in the lane loop's
+ * hand-over. */
+__device__ __forceinline__ void early_child_push(const Ctl &C, const double x[4], const double k[4], const Rng &rng,
+                                                 int n_scatt, const Cold *cold, const Fluid &F, double wc) {
+    SReq R;
+    make_sreq(R, x, k, rng, n_scatt, cold, F, wc);
+    if (__hip_atomic_load(C.early_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < C.early_cap) {
+        const unsigned long long slot = atomicAdd(C.early_tail, 1ull);
+        if (slot < C.early_cap) {
+            LoneRec *r = C.early_q + slot;
+            store_sreq(reinterpret_cast<SReq *>(r), R);
+            r->pad = 1;
+            atomicAdd(C.early_kids, 1ull);
+            __threadfence();
+            __hip_atomic_store(C.early_ready + slot, C.early_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
     push_overflow_req(C, R);
 }
 
@@ -1249,7 +1281,8 @@ __device__ __forceinline__ bool lone_stop(const Params &P, double x1, double &w,
 
 /* The interaction wave of a pair: one handed-over photon, from its record to its end (the
  * geometry wave is started on it with a restart request: generation gen + 1, step 0). */
-__device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, int lane, LonePair &pr, unsigned &gen_io) {
+__device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, int lane, LonePair &pr, unsigned &gen_io,
+                              bool kids) {
     double x1 = R.x[1];
     unsigned gen = gen_io + 1;
     if (lane == 0) {
@@ -1556,8 +1589,15 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
                     double a_s2 = 0.0, a_a2 = 0.0;
                     if (!(nu2 < 0.0)) radiation_coeffs(P, k, F, nu2, a_s2, a_a2);
                     const double bf2 = bias_func(bias_d, F.theta_e, w);
-                    if (F.n_e > 0.0) { /* the child (:1015-1024): to the overflow pool, tracked by the relaunch */
-                        if (own) push_overflow(C, x, k, rng, n_scatt, cold, F, wc);
+                    if (F.n_e > 0.0) {
+                        /* the child (:1015-1024): on the early worker into its queue, tracked by the
+                         * next free pair; else to the overflow pool, tracked by the relaunch */
+                        if (own) {
+                            if (kids)
+                                early_child_push(C, x, k, rng, n_scatt, cold, F, wc);
+                            else
+                                push_overflow(C, x, k, rng, n_scatt, cold, F, wc);
+                        }
                         ++children;
                     }
                     a_si = a_s2;
@@ -1671,7 +1711,7 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
         return;
     }
     unsigned gen = 0;
-    lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen);
+    lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen, false);
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -1682,21 +1722,115 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
  * waits for them to be published and tracks them with its geometry wave.  It exits once the bulk
  * launch has ended (early_done, set by its last workgroup) and every claimed slot is done.  Without
  * it such a photon would advance one step per lane-loop trip (~7 us) until the bulk ends. */
+/* A child request in early-queue slot r (early_child_push) made a photon at the top of its first
+ * step: scatter_super_photon's sampling and the set-up at the head of track_super_photon
+ * (harm_model.cpp:1083-1215, 895-917) -- the lane loop's sample_child, init_photon and set-up trip,
+ * with the same functions: dk/dlambda from the connection at x (its zero-length push), the fluid,
+ * both coefficients and the bias at x -- written back into the slot as the LoneRec a hand-over would
+ * be.  The whole wave, identical values in every lane; lane 0 writes.  false = an invalid child
+ * (traced with reason 4, as in the lane loop). */
+/* out of line: inlined, it changed the whole early kernel's register allocation and the serial chain
+ * ran 1.306-1.313 us/step against 1.299-1.307 (HEAD's build 1.292-1.299; tools/gpu_kids_ab.sh) */
+__device__ __attribute__((noinline)) bool early_child_setup(const Params &P, const Ctl &C, LoneRec *r, int lane) {
+    SReq R;
+    load_sreq(reinterpret_cast<const SReq *>(r), R);
+    Rng rng;
+    rng.k0 = C.key0;
+    rng.k1 = C.key1;
+    double x[4], k[4], w;
+    Cold c;
+    if (lane == 0) atomicAdd(&C.ctr->n_tracked, 1ull);
+    bool ok = sample_child_core(P, R, rng, x, k, w, &c);
+    ok = ok && !(isnan(x[0]) || isnan(x[1]) || isnan(x[2]) || isnan(x[3]) || isnan(k[0]) || isnan(k[1]) ||
+                 isnan(k[2]) || isnan(k[3]) || w == 0.0);
+    if (!ok) {
+        /* both of the lane loop's invalid-child traces carry these values (id, weight, x of the
+         * request, no steps) */
+        if (lane == 0 && C.trace)
+            write_trace(C, &c, R.id, R.w, R.x[1], R.x[2], R.x[3], 0.0, 0.0, R.n_scatt, 0, 4, -1, -1);
+        return false;
+    }
+    Trig T;
+    trig_at(P, x, T);
+    Gcov G;
+    gcov_from_trig(P, T, G);
+    double dk[4];
+    {
+        Conn Cn;
+        connection(P, T, Cn);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dk[i] = geo_rhs(Cn, i, k);
+    }
+    ZoneFetch Z;
+    zone_fetch(P, x, Z);
+    Fluid F;
+    fluid_from(P, x, G, Z, F);
+    const double nu = fluid_nu(k, F);
+    double a_s = 0.0, a_a = 0.0;
+    radiation_coeffs(P, k, F, nu, a_s, a_a); /* the set-up evaluates them whatever nu (transport_trip) */
+    const double bf = bias_func(bias_den(P, C), F.theta_e, w);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            r->x[i] = x[i];
+            r->k[i] = k[i];
+            r->dk[i] = dk[i];
+        }
+        r->w = w;
+        r->e_0_s = c.e;
+        r->tau_abs = 0.0;
+        r->tau_scatt = 0.0;
+        r->a_si = a_s;
+        r->a_ai = a_a;
+        r->bi = bf;
+        r->fl_ne = F.n_e;
+        r->c = c;
+        r->id = rng.id;
+        r->ctr = rng.ctr;
+        r->n_step = 0;
+        r->n_scatt = R.n_scatt;
+        r->pad = 0;
+    }
+    __threadfence(); /* the wave reads the record back (lone_interact) */
+    return true;
+}
+
 /* the early worker's next queue slot for the calling interaction wave, or ~0 when none will come.
  * Out of line (it touches only global memory): the kernel's SGPR spills 344 -> 265 */
 __device__ __attribute__((noinline)) unsigned long long early_claim(const Ctl &C, unsigned long long rt_start) {
     unsigned long long slot = 0;
     if ((threadIdx.x & 63) == 0) slot = atomicAdd(C.early_head, 1ull);
     slot = (unsigned long long)__builtin_amdgcn_readfirstlane((int)slot); /* < 2^31 */
+    unsigned long long t_done = 0; /* when this wave first saw the bulk launch ended */
     while (true) {
         if (slot < C.early_cap &&
             __hip_atomic_load(C.early_ready + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == C.early_tag)
             return slot;
         if (__hip_atomic_load(C.early_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0) {
             /* the bulk launch has ended: every claimed hand-over is published, so a slot past the
-             * claims (or past the queue) will never come */
+             * claims (or past the queue) will never come -- unless a pair still tracking a photon may
+             * append a child (early_child_push).  Slots finish in any order, but while this slot is
+             * unpublished every later one is too, so *early_fin >= slot says that every slot before
+             * it is finished: nothing is left that could append.  *early_fin is read before the tail
+             * (a pair appends before it counts its slot finished), and a pair that leaves counts its
+             * own slot, so the pair holding the next one can leave in turn. */
+            if (slot >= C.early_cap) return ~0ull;
+            const unsigned long long fin =
+                C.early_kids_on ? __hip_atomic_load(C.early_fin, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : 0;
             const unsigned long long tail = __hip_atomic_load(C.early_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (slot >= tail || slot >= C.early_cap) return ~0ull;
+            if (slot >= tail && (!C.early_kids_on || fin >= slot)) {
+                if (C.early_kids_on && (threadIdx.x & 63) == 0)
+                    __hip_atomic_fetch_add(C.early_fin, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                return ~0ull;
+            }
+            /* a guard, not a path: the other pair's photon ends within its own watchdog; a count
+             * that never arrives (a bug) fails the call instead of keeping the GPU */
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (t_done == 0) t_done = now;
+            if (now - t_done > 2 * (C.watchdog_ticks ? C.watchdog_ticks : 6000000000ull)) {
+                if ((threadIdx.x & 63) == 0) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return ~0ull;
+            }
         }
         if (__builtin_amdgcn_s_memrealtime() - rt_start > EARLY_ALONE_TICKS &&
             __builtin_amdgcn_readfirstlane(
@@ -1741,7 +1875,12 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
     while (true) {
         const unsigned long long slot = early_claim(C, rt_start);
         if (slot == ~0ull) break;
-        lone_interact(P, C, C.early_q[slot], lane, pr, gen);
+        LoneRec *r = C.early_q + slot;
+        /* a child request (pad = 1, wave-uniform) becomes a photon at the top of its first step */
+        const bool go = r->pad != 1 || early_child_setup(P, C, r, lane);
+        if (go) lone_interact(P, C, *r, lane, pr, gen, C.early_kids_on != 0);
+        if (C.early_kids_on && lane == 0)
+            __hip_atomic_fetch_add(C.early_fin, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -2587,6 +2726,7 @@ struct grm_engine {
         return s > (double)(1 << 30) ? (1 << 30) : (int)s;
     }
     bool early_serial = false; /* test: the worker ahead of the main launch on its stream */
+    int early_children = 1;    /* GRM_OPT_EARLY_CHILDREN: the worker tracks its photons' children itself */
     int karg_test = 0;         /* test: GRM_OPT_KARG_TEST */
     static constexpr unsigned long long EARLY_CAP = 1024;
     LoneRec *d_early = nullptr;
@@ -2862,9 +3002,10 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             op.warm_val = h * WARM_HIST;
         }
         /* the main launch runs the early worker beside it: [8] early tail, [9] head, [10] done,
-         * [11] workgroups exited, [12] worker running / closed, [13] bulk started */
+         * [11] workgroups exited, [12] worker running / closed, [13] bulk started, [14] slots
+         * finished, [15] the worker's children in its queue */
         const bool early = pass == 0 && C.pool_kind == 0 && e->early_steps > 0 && !C.lone_all && grid > 1;
-        if (early) op.set |= 0x3f00u;
+        if (early) op.set |= 0xff00u;
         if (ctl(e, op, false)) return -1;
         if (early) {
             C.early_q = e->d_early;
@@ -2878,8 +3019,12 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.early_live = e->d_small + (12) * SMALL_STRIDE;
             C.bulk_live = e->d_small + (13) * SMALL_STRIDE;
             C.early_steps = grm_engine::early_steps_for(e->early_steps, n);
+            C.early_kids_on = e->early_children;
+            C.early_fin = e->d_small + (14) * SMALL_STRIDE;
+            C.early_kids = e->d_small + (15) * SMALL_STRIDE;
         } else {
             C.early_q = nullptr;
+            C.early_kids_on = 0;
         }
         C.ovf = e->d_ovf[dst];
         C.ovf_count = e->d_small + (1 + dst) * SMALL_STRIDE;
@@ -2939,7 +3084,11 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
         ms_total += ms;
         const unsigned long long n_lone = std::min<unsigned long long>(e->pin->small[7], e->lone_cap);
-        if (early) e->stats.n_early += std::min<unsigned long long>(e->pin->small[8], grm_engine::EARLY_CAP);
+        if (early) { /* the published slots: hand-overs and the worker's own children */
+            const unsigned long long kids = e->pin->small[15];
+            e->stats.n_early += std::min<unsigned long long>(e->pin->small[8], grm_engine::EARLY_CAP) - kids;
+            e->stats.n_early_children += kids;
+        }
         if (early && !e->early_serial) { /* ev_pre (engine stream, before the bulk) .. ev_w (after the worker) */
             float ms_e = 0.f;
             HIPCHK(e, hipEventElapsedTime(&ms_e, e->ev_pre, e->ev_w));
@@ -3252,6 +3401,7 @@ int grm_engine_set_option(grm_engine *e, int opt, int64_t v) {
     case GRM_OPT_WARMUP_SPREAD: e->warmup_spread = v < 0 ? -1 : v; return 0;
     case GRM_OPT_EARLY_STEPS: e->early_steps = v < 0 ? 0 : (v > (1 << 30) ? (1 << 30) : (int)v); return 0;
     case GRM_OPT_EARLY_SERIAL: e->early_serial = v != 0; return 0;
+    case GRM_OPT_EARLY_CHILDREN: e->early_children = v != 0; return 0;
     case GRM_OPT_KARG_TEST: e->karg_test = (int)v; return 0;
     case GRM_OPT_WATCHDOG_MS: e->watchdog_ms = v < 0 ? 0 : v; return 0;
 #ifdef GRM_WITH_SPLIT

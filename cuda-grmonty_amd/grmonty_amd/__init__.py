@@ -57,6 +57,7 @@ OPT_KARG_TEST = 17
 OPT_WARMUP_SPREAD = 19
 OPT_FLIGHT_RATIO = 22
 OPT_JOB_START_WAIT_MS = 28
+OPT_EARLY_CHILDREN = 29
 OPT_SPLIT, OPT_SPLIT_THR, OPT_SPLIT_SPIN, OPT_SPLIT_GTHR, OPT_SPLIT_BATCH = 23, 24, 25, 26, 27
 N_TH_BINS, N_E_BINS = 6, 200
 
@@ -83,7 +84,8 @@ class Stats(C.Structure):
                 ("max_launch_ms", C.c_double), ("max_launch_steps", C.c_uint64),
                 ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64), ("n_abandoned", C.c_uint64),
                 ("n_nan_photons", C.c_uint64), ("n_lone", C.c_uint64), ("lone_ms", C.c_double),
-                ("n_early", C.c_uint64), ("early_ms", C.c_double), ("last_grid", C.c_uint64)]
+                ("n_early", C.c_uint64), ("early_ms", C.c_double), ("last_grid", C.c_uint64),
+                ("n_early_children", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

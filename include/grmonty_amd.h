@@ -122,6 +122,7 @@ typedef struct grm_stats {
     uint64_t n_early;          /* long photons handed to the concurrent early worker since the last reset */
     double early_ms;           /* the early worker's longest launch (its stream's events) since the last reset */
     uint64_t last_grid;        /* workgroups of the most recent transport call's launch (GRM_OPT_FLIGHT_RATIO) */
+    uint64_t n_early_children; /* scattered children the early worker tracked itself (GRM_OPT_EARLY_CHILDREN) */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
@@ -201,7 +202,12 @@ enum {
      * that no rank begins the job's warm-up alone (default 0 = no wait: ranks that run their passes
      * back to back stay uncoupled; the one-GPU emulation of N ranks, whose launches queue behind each
      * other, sets 500) */
-    GRM_OPT_JOB_START_WAIT_MS = 28
+    GRM_OPT_JOB_START_WAIT_MS = 28,
+    /* 1 (default): the scattered child of a photon on the early worker (GRM_OPT_EARLY_STEPS) joins the
+     * worker's queue and starts on the next free pair at once -- the reference tracks a child as soon
+     * as it is made (harm_model.cpp:1016-1023) -- instead of waiting for the overflow relaunch after
+     * the worker has ended; 0: every such child goes to the overflow relaunch */
+    GRM_OPT_EARLY_CHILDREN = 29
 };
 
 /* --- engine lifecycle (super_photon.cuh:29-40) ------------------------------------------ */

@@ -48,7 +48,8 @@ def _has_split():
         return False
 
 
-_PATHS = [(1, "lane-loop"), (2, "lone-kernel"), (3, "early-worker"), (4, "early-serialised")]
+_PATHS = [(1, "lane-loop"), (2, "lone-kernel"), (3, "early-worker"), (4, "early-serialised"),
+          (8, "early-worker-children-relaunched"), (9, "early-worker-children")]
 if _has_split():
     _PATHS += [(5, "split"), (6, "split-early"), (7, "split-by-simd")]
 
@@ -59,15 +60,21 @@ def test_photon_by_photon(setup, oracle64, lone):
     over the lanes) at the top of its first step; lone=3 hands every photon that reaches 40 steps to
     the concurrent early worker (up to its queue's 1024); lone=4 runs that worker ahead of the main
     launch on its stream, as a kernel-serialising profiler would, so it must leave and take none;
+    lone=8 is lone=3 with the worker's own children sent to the overflow relaunch
+    (GRM_OPT_EARLY_CHILDREN = 0) instead of tracked by the worker's next free pair (lone=3, whose
+    queue the hand-overs fill); lone=9 hands over at 300 steps (~285 lives reach it, oracle trace of
+    this selection), so the queue keeps room for the workers' own children and grandchildren;
     lone=5 runs the bulk as split_kernel (geometry and interaction waves, grm_split.hip), lone=6 that
     kernel handing photons of 40 steps to the early worker, lone=7 that kernel with the roles dealt by
     SIMD (GRM_OPT_SPLIT = 2): those paths against the oracle"""
     G, O, sel, snap, eng = setup
-    if lone >= 5:
+    split = 5 <= lone <= 7
+    if split:
         eng.set_option(G.OPT_SPLIT, 2 if lone == 7 else 1)
-    eng.set_option(G.OPT_WATCHDOG_MS, 20000 if lone >= 5 else 60000)
+    eng.set_option(G.OPT_WATCHDOG_MS, 20000 if split else 60000)
     eng.set_option(G.OPT_LONE, 1 if lone >= 3 else lone)
-    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone in (3, 4, 6) else 1500)
+    eng.set_option(G.OPT_EARLY_STEPS, 40 if lone in (3, 4, 6, 8) else 300 if lone == 9 else 1500)
+    eng.set_option(G.OPT_EARLY_CHILDREN, 0 if lone == 8 else 1)
     eng.set_option(G.OPT_EARLY_SERIAL, 1 if lone == 4 else 0)
     oracle64.reset()
     tr_o = oracle64.track(sel, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=snap["scatt"],
@@ -90,13 +97,22 @@ def test_photon_by_photon(setup, oracle64, lone):
     eng.set_option(G.OPT_LONE, 1)
     eng.set_option(G.OPT_EARLY_STEPS, 1500)
     eng.set_option(G.OPT_EARLY_SERIAL, 0)
-    if lone >= 5:
+    eng.set_option(G.OPT_EARLY_CHILDREN, 1)
+    if split:
         eng.set_option(G.OPT_SPLIT, 0)
     eng.set_option(G.OPT_WATCHDOG_MS, 60000)
     if lone == 2:
         assert st["n_lone"] >= len(sel) // 2, st["n_lone"]
-    if lone in (3, 6):
+    if lone in (3, 6, 8):
         assert st["n_early"] >= 200, st["n_early"]
+    print(f"early worker: {st['n_early']} hand-overs, {st['n_early_children']} of their children tracked "
+          f"on it, overflow {st['n_overflow']}")
+    if lone == 3:
+        assert st["n_early_children"] > 0, st["n_early_children"]
+    if lone == 9:
+        assert st["n_early"] >= 100 and st["n_early_children"] >= 20, (st["n_early"], st["n_early_children"])
+    if lone in (4, 8):
+        assert st["n_early_children"] == 0, st["n_early_children"]
     if lone == 4:
         assert st["n_early"] == 0, st["n_early"]
     assert st["n_dropped"] == 0
