@@ -171,11 +171,19 @@ struct Ctl {
     int split_mode; /* 1: waves 0-3 geometry, 4-7 interaction; 2: roles by the SIMD a wave runs on */
     int split_batch; /* consecutive ready slots an interaction lane may evaluate per round */
     /* the early worker's own children (GRM_OPT_EARLY_CHILDREN): a scattering on a pair appends the
-     * child's scatter request to the early queue (LoneRec::pad = 1, early_child_push), where the next
-     * free pair sets it up and tracks it (early_child_setup); *early_fin counts the queue slots
+     * child's scatter request to the early queue (LoneRec::pad = 1, queue_child_push), where the next
+     * free pair sets it up and tracks it (child_setup_body); *early_fin counts the queue slots
      * finished -- tracked, or given up by a pair that left -- and *early_kids the children appended */
     int early_kids_on;
     unsigned long long *early_fin, *early_kids;
+    /* the lone kernel's own children (the same option): a scattering on a lone pair appends the child's
+     * request to lk_q (lk_tail; published by lk_ready[slot] = lk_tag), which the pairs that have
+     * finished their photon take in order (lk_taken); lk_active counts the pairs tracking a photon
+     * and lk_standby those waiting for a child (at most LK_STANDBY wait; the rest leave) */
+    int lk_on;
+    LoneRec *lk_q;
+    unsigned long long *lk_ready, lk_cap, lk_tag;
+    unsigned long long *lk_tail, *lk_taken, *lk_active, *lk_standby;
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -969,23 +977,29 @@ __device__ __forceinline__ void push_overflow(const Ctl &C, const double x[4], c
 
 /* the child of an early-worker photon's scattering (lane 0): its scatter request goes into a slot of
  * the early queue, marked as a request (LoneRec::pad = 1; the SReq fills the slot's first 192 B), and
- * the next free pair of the worker sets it up and tracks it at once (early_child_setup), as the
+ * the next free pair of the worker sets it up and tracks it at once (child_setup_body), as the
  * reference tracks a child as soon as it is made (harm_model.cpp:1016-1023); the overflow pool when
  * the queue is full.  A slot claimed past the cap is never published, as in the lane loop's
  * hand-over. */
-__device__ __forceinline__ void early_child_push(const Ctl &C, const double x[4], const double k[4], const Rng &rng,
-                                                 int n_scatt, const Cold *cold, const Fluid &F, double wc) {
+/* kids: 1 the early worker's queue, 2 the lone kernel's (lk_q; its slots are all requests) */
+__device__ __forceinline__ void queue_child_push(const Ctl &C, int kids, const double x[4], const double k[4],
+                                                 const Rng &rng, int n_scatt, const Cold *cold, const Fluid &F,
+                                                 double wc) {
     SReq R;
     make_sreq(R, x, k, rng, n_scatt, cold, F, wc);
-    if (__hip_atomic_load(C.early_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < C.early_cap) {
-        const unsigned long long slot = atomicAdd(C.early_tail, 1ull);
-        if (slot < C.early_cap) {
-            LoneRec *r = C.early_q + slot;
+    LoneRec *q = kids == 1 ? C.early_q : C.lk_q;
+    unsigned long long *ready = kids == 1 ? C.early_ready : C.lk_ready;
+    unsigned long long *tail = kids == 1 ? C.early_tail : C.lk_tail;
+    const unsigned long long cap = kids == 1 ? C.early_cap : C.lk_cap, tag = kids == 1 ? C.early_tag : C.lk_tag;
+    if (__hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cap) {
+        const unsigned long long slot = atomicAdd(tail, 1ull);
+        if (slot < cap) {
+            LoneRec *r = q + slot;
             store_sreq(reinterpret_cast<SReq *>(r), R);
             r->pad = 1;
-            atomicAdd(C.early_kids, 1ull);
+            if (kids == 1) atomicAdd(C.early_kids, 1ull);
             __threadfence();
-            __hip_atomic_store(C.early_ready + slot, C.early_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ready + slot, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
     }
@@ -1281,8 +1295,10 @@ __device__ __forceinline__ bool lone_stop(const Params &P, double x1, double &w,
 
 /* The interaction wave of a pair: one handed-over photon, from its record to its end (the
  * geometry wave is started on it with a restart request: generation gen + 1, step 0). */
+/* kids: where the photon's scattered children go -- 0 the overflow pool, 1 the early worker's queue,
+ * 2 the lone kernel's (queue_child_push) */
 __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, int lane, LonePair &pr, unsigned &gen_io,
-                              bool kids) {
+                              int kids) {
     double x1 = R.x[1];
     unsigned gen = gen_io + 1;
     if (lane == 0) {
@@ -1594,7 +1610,7 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
                          * next free pair; else to the overflow pool, tracked by the relaunch */
                         if (own) {
                             if (kids)
-                                early_child_push(C, x, k, rng, n_scatt, cold, F, wc);
+                                queue_child_push(C, kids, x, k, rng, n_scatt, cold, F, wc);
                             else
                                 push_overflow(C, x, k, rng, n_scatt, cold, F, wc);
                         }
@@ -1692,6 +1708,72 @@ __device__ void lone_interact(const Params &P, const Ctl &C, const LoneRec &R, i
 }
 
 #ifdef GRM_LONE_TU
+__device__ __forceinline__ bool child_setup_body(const Params &P, const Ctl &C, LoneRec *r, int lane);
+
+constexpr unsigned long long LK_STANDBY = 4; /* lone pairs that wait for children once their photon has ended */
+#ifndef GRM_LK_SLEEP
+#define GRM_LK_SLEEP 32
+#endif
+
+/* A lone pair after its own photon (GRM_OPT_EARLY_CHILDREN): the children the kernel's photons append
+ * to lk_q, taken in order by whichever pair looks first, for as long as any pair still tracks a
+ * photon (*lk_active), so that a long photon's child starts at once instead of in the relaunch after
+ * the kernel.  A pair that finds the queue empty waits, up to LK_STANDBY pairs, or leaves.  Leaving
+ * is safe whenever the queue is empty: a child is only appended by a pair that is tracking, and
+ * every pair looks at the queue again when its photon ends.  Whole wave, uniform control. */
+__device__ void lone_children(const Params &P, const Ctl &C, int lane, LonePair &pr, unsigned &gen) {
+    bool standing = false;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+        const unsigned long long act = __hip_atomic_load(C.lk_active, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long taken = __hip_atomic_load(C.lk_taken, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long tail = __hip_atomic_load(C.lk_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (tail > C.lk_cap) tail = C.lk_cap;
+        if (taken < tail) {
+            /* counted as tracking before the claim, so that no waiting pair leaves in between */
+            unsigned long long got = ~0ull;
+            if (lane == 0) {
+                atomicAdd(C.lk_active, 1ull);
+                unsigned long long want = taken;
+                if (__hip_atomic_compare_exchange_strong(C.lk_taken, &want, taken + 1, __ATOMIC_ACQ_REL,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    got = taken;
+                else
+                    atomicAdd(C.lk_active, ~0ull);
+            }
+            got = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(got >> 32)) << 32) |
+                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)got);
+            if (got == ~0ull) continue;
+            if (standing && lane == 0) atomicAdd(C.lk_standby, ~0ull);
+            standing = false;
+            while (__hip_atomic_load(C.lk_ready + got, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.lk_tag)
+                __builtin_amdgcn_s_sleep(1);
+            LoneRec *r = C.lk_q + got;
+            if (child_setup_body(P, C, r, lane)) lone_interact(P, C, *r, lane, pr, gen, 2);
+            if (lane == 0) __hip_atomic_fetch_add(C.lk_active, ~0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        if (act == 0) break; /* nothing queued and nothing tracked: no child can come */
+        if (!standing) {
+            unsigned long long sb = 0;
+            if (lane == 0) sb = atomicAdd(C.lk_standby, 1ull);
+            sb = (unsigned long long)__builtin_amdgcn_readfirstlane((int)sb);
+            if (sb >= LK_STANDBY) {
+                if (lane == 0) atomicAdd(C.lk_standby, ~0ull);
+                return;
+            }
+            standing = true;
+        }
+        /* a guard, not a path: every tracked photon ends within its own watchdog */
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * (C.watchdog_ticks ? C.watchdog_ticks : 6000000000ull)) {
+            if (lane == 0) __hip_atomic_store(&C.ctr->abort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(GRM_LK_SLEEP);
+    }
+    if (standing && lane == 0) atomicAdd(C.lk_standby, ~0ull);
+}
+
 /* launched on lone_cap workgroups; the launch before handed over *C.lone_count photons */
 __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
     const unsigned long long n_handed = __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1711,7 +1793,12 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
         return;
     }
     unsigned gen = 0;
-    lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen, false);
+    if (C.lk_on && lane == 0) atomicAdd(C.lk_active, 1ull);
+    lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen, C.lk_on ? 2 : 0);
+    if (C.lk_on) {
+        if (lane == 0) __hip_atomic_fetch_add(C.lk_active, ~0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        lone_children(P, C, lane, pr, gen);
+    }
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -1722,16 +1809,18 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
  * waits for them to be published and tracks them with its geometry wave.  It exits once the bulk
  * launch has ended (early_done, set by its last workgroup) and every claimed slot is done.  Without
  * it such a photon would advance one step per lane-loop trip (~7 us) until the bulk ends. */
-/* A child request in early-queue slot r (early_child_push) made a photon at the top of its first
+/* A child request in a queue slot r (queue_child_push) made a photon at the top of its first
  * step: scatter_super_photon's sampling and the set-up at the head of track_super_photon
  * (harm_model.cpp:1083-1215, 895-917) -- the lane loop's sample_child, init_photon and set-up trip,
  * with the same functions: dk/dlambda from the connection at x (its zero-length push), the fluid,
  * both coefficients and the bias at x -- written back into the slot as the LoneRec a hand-over would
  * be.  The whole wave, identical values in every lane; lane 0 writes.  false = an invalid child
  * (traced with reason 4, as in the lane loop). */
-/* out of line: inlined, it changed the whole early kernel's register allocation and the serial chain
- * ran 1.306-1.313 us/step against 1.299-1.307 (HEAD's build 1.292-1.299; tools/gpu_kids_ab.sh) */
-__device__ __attribute__((noinline)) bool early_child_setup(const Params &P, const Ctl &C, LoneRec *r, int lane) {
+/* Inlined.  Out of line (a call) the early kernel's serial chain ran 1.299-1.307 us/step against
+ * 1.306-1.313 inlined (tools/gpu_kids_ab.sh), but the same call from lone_kernel handed lone_interact
+ * records whose weight came out NaN (every child of the lone kernel's photons; profiles/
+ * r06_early_children/lk_debug.log) while the inlined body is photon-by-photon exact in both kernels. */
+__device__ __forceinline__ bool child_setup_body(const Params &P, const Ctl &C, LoneRec *r, int lane) {
     SReq R;
     load_sreq(reinterpret_cast<const SReq *>(r), R);
     Rng rng;
@@ -1809,7 +1898,7 @@ __device__ __attribute__((noinline)) unsigned long long early_claim(const Ctl &C
         if (__hip_atomic_load(C.early_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0) {
             /* the bulk launch has ended: every claimed hand-over is published, so a slot past the
              * claims (or past the queue) will never come -- unless a pair still tracking a photon may
-             * append a child (early_child_push).  Slots finish in any order, but while this slot is
+             * append a child (queue_child_push).  Slots finish in any order, but while this slot is
              * unpublished every later one is too, so *early_fin >= slot says that every slot before
              * it is finished: nothing is left that could append.  *early_fin is read before the tail
              * (a pair appends before it counts its slot finished), and a pair that leaves counts its
@@ -1877,8 +1966,8 @@ __global__ __launch_bounds__(64 * 2 * LONE_PAIRS) void early_kernel(Params P, Ct
         if (slot == ~0ull) break;
         LoneRec *r = C.early_q + slot;
         /* a child request (pad = 1, wave-uniform) becomes a photon at the top of its first step */
-        const bool go = r->pad != 1 || early_child_setup(P, C, r, lane);
-        if (go) lone_interact(P, C, *r, lane, pr, gen, C.early_kids_on != 0);
+        const bool go = r->pad != 1 || child_setup_body(P, C, r, lane);
+        if (go) lone_interact(P, C, *r, lane, pr, gen, C.early_kids_on ? 1 : 0);
         if (C.early_kids_on && lane == 0)
             __hip_atomic_fetch_add(C.early_fin, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2731,6 +2820,11 @@ struct grm_engine {
     static constexpr unsigned long long EARLY_CAP = 1024;
     LoneRec *d_early = nullptr;
     unsigned long long *d_early_ready = nullptr;
+    /* the lone kernel's children queue (Ctl::lk_*): LK_CAP slots, their ready tags, and the four words
+     * tail, taken, active, standby (one per SMALL_STRIDE), cleared before every lone launch */
+    static constexpr unsigned long long LK_CAP = 4096;
+    LoneRec *d_lk = nullptr;
+    unsigned long long *d_lk_ready = nullptr, *d_lk_words = nullptr;
     unsigned long long launch_seq = 0;
     size_t waves_rows = 0; /* rows of d_waves the last recorded launch wrote */
     hipStream_t stream2 = nullptr;
@@ -3073,6 +3167,18 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
         /* the photons the launch handed over (a count on the device), one wave pair each; their
          * children join this launch's overflow pool */
         if (C.lone) {
+            /* the lone pairs track the children of their photons themselves (GRM_OPT_EARLY_CHILDREN) */
+            C.lk_on = e->early_children;
+            C.lk_q = e->d_lk;
+            C.lk_ready = e->d_lk_ready;
+            C.lk_cap = grm_engine::LK_CAP;
+            C.lk_tag = ++e->launch_seq;
+            C.lk_tail = e->d_lk_words + 0 * SMALL_STRIDE;
+            C.lk_taken = e->d_lk_words + 1 * SMALL_STRIDE;
+            C.lk_active = e->d_lk_words + 2 * SMALL_STRIDE;
+            C.lk_standby = e->d_lk_words + 3 * SMALL_STRIDE;
+            if (C.lk_on)
+                HIPCHK(e, hipMemsetAsync(e->d_lk_words, 0, 4 * SMALL_STRIDE * sizeof(unsigned long long), e->stream));
             HIPCHK(e, hipEventRecord(e->ev2, e->stream));
             HIPCHK(e, grm_lone_launch(0, (unsigned)e->lone_cap, e->stream, &e->P, sizeof(Params), &C, sizeof(Ctl)));
             HIPCHK(e, hipEventRecord(e->ev3, e->stream));
@@ -3100,6 +3206,11 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             ms_total += ms_l;
             e->stats.lone_ms += ms_l;
             e->stats.n_lone += n_lone;
+            if (C.lk_on) {
+                unsigned long long lk_tail = 0;
+                HIPCHK(e, hipMemcpy(&lk_tail, e->d_lk_words, sizeof(lk_tail), hipMemcpyDeviceToHost));
+                e->stats.n_lone_children += std::min<unsigned long long>(lk_tail, grm_engine::LK_CAP);
+            }
             if (n_lone) e->stats.n_launches++;
         }
         const unsigned long long cnt = e->pin->small[1 + dst];
@@ -3238,7 +3349,11 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
         !hip_ok(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking), "stream") ||
         !hip_ok(e, hipMalloc(&e->d_early, grm_engine::EARLY_CAP * sizeof(LoneRec)), "early queue") ||
         !hip_ok(e, hipMalloc(&e->d_early_ready, grm_engine::EARLY_CAP * sizeof(unsigned long long)), "early queue") ||
-        !hip_ok(e, hipMemset(e->d_early_ready, 0, grm_engine::EARLY_CAP * sizeof(unsigned long long)), "early queue"))
+        !hip_ok(e, hipMemset(e->d_early_ready, 0, grm_engine::EARLY_CAP * sizeof(unsigned long long)), "early queue") ||
+        !hip_ok(e, hipMalloc(&e->d_lk, grm_engine::LK_CAP * sizeof(LoneRec)), "lone children queue") ||
+        !hip_ok(e, hipMalloc(&e->d_lk_ready, grm_engine::LK_CAP * sizeof(unsigned long long)), "lone children queue") ||
+        !hip_ok(e, hipMemset(e->d_lk_ready, 0, grm_engine::LK_CAP * sizeof(unsigned long long)), "lone children queue") ||
+        !hip_ok(e, hipMalloc(&e->d_lk_words, 4 * SMALL_STRIDE * sizeof(unsigned long long)), "lone children queue"))
         return fail();
     if (!hip_ok(e, hipHostMalloc(reinterpret_cast<void **>(&e->pin), sizeof(grm_engine::Pinned),
                                  hipHostMallocMapped | hipHostMallocCoherent),
@@ -3364,6 +3479,9 @@ void grm_engine_destroy(grm_engine *e) {
     if (e->stream2) hipStreamDestroy(e->stream2);
     hipFree(e->d_early);
     hipFree(e->d_early_ready);
+    hipFree(e->d_lk);
+    hipFree(e->d_lk_ready);
+    hipFree(e->d_lk_words);
     if (e->stream) hipStreamDestroy(e->stream);
     delete e;
 }

@@ -85,7 +85,7 @@ class Stats(C.Structure):
                 ("max_photon_steps", C.c_uint64), ("n_long_photons", C.c_uint64), ("n_abandoned", C.c_uint64),
                 ("n_nan_photons", C.c_uint64), ("n_lone", C.c_uint64), ("lone_ms", C.c_double),
                 ("n_early", C.c_uint64), ("early_ms", C.c_double), ("last_grid", C.c_uint64),
-                ("n_early_children", C.c_uint64)]
+                ("n_early_children", C.c_uint64), ("n_lone_children", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

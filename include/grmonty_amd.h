@@ -123,6 +123,7 @@ typedef struct grm_stats {
     double early_ms;           /* the early worker's longest launch (its stream's events) since the last reset */
     uint64_t last_grid;        /* workgroups of the most recent transport call's launch (GRM_OPT_FLIGHT_RATIO) */
     uint64_t n_early_children; /* scattered children the early worker tracked itself (GRM_OPT_EARLY_CHILDREN) */
+    uint64_t n_lone_children;  /* scattered children the lone kernel tracked itself (GRM_OPT_EARLY_CHILDREN) */
 } grm_stats;
 
 typedef struct grm_engine grm_engine;
@@ -203,10 +204,11 @@ enum {
      * back to back stay uncoupled; the one-GPU emulation of N ranks, whose launches queue behind each
      * other, sets 500) */
     GRM_OPT_JOB_START_WAIT_MS = 28,
-    /* 1 (default): the scattered child of a photon on the early worker (GRM_OPT_EARLY_STEPS) joins the
-     * worker's queue and starts on the next free pair at once -- the reference tracks a child as soon
-     * as it is made (harm_model.cpp:1016-1023) -- instead of waiting for the overflow relaunch after
-     * the worker has ended; 0: every such child goes to the overflow relaunch */
+    /* 1 (default): the scattered child of a photon on a two-wave pair -- the early worker's
+     * (GRM_OPT_EARLY_STEPS) or the lone kernel's (GRM_OPT_LONE) -- joins that kernel's queue of
+     * children and starts on its next free pair at once, as the reference tracks a child as soon as
+     * it is made (harm_model.cpp:1016-1023), instead of waiting for the overflow relaunch after the
+     * kernel has ended; 0: every such child goes to the overflow relaunch */
     GRM_OPT_EARLY_CHILDREN = 29
 };
 

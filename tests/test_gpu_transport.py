@@ -49,7 +49,8 @@ def _has_split():
 
 
 _PATHS = [(1, "lane-loop"), (2, "lone-kernel"), (3, "early-worker"), (4, "early-serialised"),
-          (8, "early-worker-children-relaunched"), (9, "early-worker-children")]
+          (8, "early-worker-children-relaunched"), (9, "early-worker-children"),
+          (10, "lone-kernel-children-relaunched")]
 if _has_split():
     _PATHS += [(5, "split"), (6, "split-early"), (7, "split-by-simd")]
 
@@ -62,7 +63,9 @@ def test_photon_by_photon(setup, oracle64, lone):
     launch on its stream, as a kernel-serialising profiler would, so it must leave and take none;
     lone=8 is lone=3 with the worker's own children sent to the overflow relaunch
     (GRM_OPT_EARLY_CHILDREN = 0) instead of tracked by the worker's next free pair (lone=3, whose
-    queue the hand-overs fill); lone=9 hands over at 300 steps (~285 lives reach it, oracle trace of
+    queue the hand-overs fill); lone=10 is lone=2 with the lone kernel's children sent to the overflow
+    relaunch (in lone=2 the pairs that have ended their photon take them from the kernel's own
+    queue); lone=9 hands over at 300 steps (~285 lives reach it, oracle trace of
     this selection), so the queue keeps room for the workers' own children and grandchildren;
     lone=5 runs the bulk as split_kernel (geometry and interaction waves, grm_split.hip), lone=6 that
     kernel handing photons of 40 steps to the early worker, lone=7 that kernel with the roles dealt by
@@ -72,9 +75,9 @@ def test_photon_by_photon(setup, oracle64, lone):
     if split:
         eng.set_option(G.OPT_SPLIT, 2 if lone == 7 else 1)
     eng.set_option(G.OPT_WATCHDOG_MS, 20000 if split else 60000)
-    eng.set_option(G.OPT_LONE, 1 if lone >= 3 else lone)
+    eng.set_option(G.OPT_LONE, 2 if lone == 10 else 1 if lone >= 3 else lone)
     eng.set_option(G.OPT_EARLY_STEPS, 40 if lone in (3, 4, 6, 8) else 300 if lone == 9 else 1500)
-    eng.set_option(G.OPT_EARLY_CHILDREN, 0 if lone == 8 else 1)
+    eng.set_option(G.OPT_EARLY_CHILDREN, 0 if lone in (8, 10) else 1)
     eng.set_option(G.OPT_EARLY_SERIAL, 1 if lone == 4 else 0)
     oracle64.reset()
     tr_o = oracle64.track(sel, rng_mode=1, seed=123, id_base=0, frozen=True, scatt0=snap["scatt"],
@@ -101,8 +104,13 @@ def test_photon_by_photon(setup, oracle64, lone):
     if split:
         eng.set_option(G.OPT_SPLIT, 0)
     eng.set_option(G.OPT_WATCHDOG_MS, 60000)
-    if lone == 2:
+    if lone in (2, 10):
         assert st["n_lone"] >= len(sel) // 2, st["n_lone"]
+    print(f"lone kernel: {st['n_lone']} photons, {st['n_lone_children']} of their children tracked in it")
+    if lone == 2:
+        assert st["n_lone_children"] > 0, st["n_lone_children"]
+    if lone == 10:
+        assert st["n_lone_children"] == 0, st["n_lone_children"]
     if lone in (3, 6, 8):
         assert st["n_early"] >= 200, st["n_early"]
     print(f"early worker: {st['n_early']} hand-overs, {st['n_early_children']} of their children tracked "

@@ -28,6 +28,8 @@ e.set_option(G.OPT_FROZEN_SCATT, SNAP["scatt"])
 e.set_option(G.OPT_FROZEN_REC, SNAP["rec"])
 e.set_option(G.OPT_FROZEN_MAXTAU, struct.unpack("<q", struct.pack("<d", SNAP["maxtau"]))[0])
 EARLY = os.environ.get("EARLY") == "1"
+for kv in os.environ.get("OPTS", "").split():  # engine options K=V (experiments)
+    e.set_option(int(kv.split("=")[0]), int(kv.split("=")[1]))
 if EARLY:
     e.set_option(G.OPT_LONE, 0)
     e.set_option(G.OPT_GRID_BLOCKS, 2)
