@@ -184,6 +184,7 @@ struct Ctl {
     LoneRec *lk_q;
     unsigned long long *lk_ready, lk_cap, lk_tag;
     unsigned long long *lk_tail, *lk_taken, *lk_active, *lk_standby;
+    unsigned long long *lk_orig; /* handed-over photons whose pair has finished them */
 };
 constexpr int STUCK_WORDS = 16, STUCK_CAP = 256;
 constexpr unsigned REFRESH_TRIPS = 64; /* counter flush + bias refresh + watchdog period (power of 2) */
@@ -1721,10 +1722,14 @@ constexpr unsigned long long LK_STANDBY = 4; /* lone pairs that wait for childre
  * the kernel.  A pair that finds the queue empty waits, up to LK_STANDBY pairs, or leaves.  Leaving
  * is safe whenever the queue is empty: a child is only appended by a pair that is tracking, and
  * every pair looks at the queue again when its photon ends.  Whole wave, uniform control. */
-__device__ void lone_children(const Params &P, const Ctl &C, int lane, LonePair &pr, unsigned &gen) {
+__device__ void lone_children(const Params &P, const Ctl &C, int lane, LonePair &pr, unsigned &gen,
+                              unsigned long long n_handed) {
     bool standing = false;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (true) {
+        /* every handed-over photon finished (its pair may not have started yet when a pair looks) */
+        const bool orig_done =
+            __hip_atomic_load(C.lk_orig, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= n_handed;
         const unsigned long long act = __hip_atomic_load(C.lk_active, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long taken = __hip_atomic_load(C.lk_taken, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long tail = __hip_atomic_load(C.lk_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
@@ -1753,7 +1758,7 @@ __device__ void lone_children(const Params &P, const Ctl &C, int lane, LonePair 
             if (lane == 0) __hip_atomic_fetch_add(C.lk_active, ~0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             continue;
         }
-        if (act == 0) break; /* nothing queued and nothing tracked: no child can come */
+        if (act == 0 && orig_done) break; /* nothing queued or tracked, nothing to come: no child can */
         if (!standing) {
             unsigned long long sb = 0;
             if (lane == 0) sb = atomicAdd(C.lk_standby, 1ull);
@@ -1774,10 +1779,16 @@ __device__ void lone_children(const Params &P, const Ctl &C, int lane, LonePair 
     if (standing && lane == 0) atomicAdd(C.lk_standby, ~0ull);
 }
 
-/* launched on lone_cap workgroups; the launch before handed over *C.lone_count photons */
+/* launched on lone_cap workgroups; the launch before handed over *C.lone_count photons, one to each of
+ * the first workgroups; with GRM_OPT_EARLY_CHILDREN the next LK_STANDBY workgroups (as the grid
+ * allows) start as standby pairs for the children, so that a launch of few photons -- a relaunch's
+ * long photon -- does not track its photons' children one after another on their own pairs */
 __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
-    const unsigned long long n_handed = __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (blockIdx.x >= n_handed || blockIdx.x >= C.lone_cap) return;
+    unsigned long long n_handed = __hip_atomic_load(C.lone_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n_handed > C.lone_cap) n_handed = C.lone_cap;
+    const bool extra = blockIdx.x >= n_handed;
+    if (blockIdx.x >= C.lone_cap || (extra && (!C.lk_on || n_handed == 0 || blockIdx.x >= n_handed + LK_STANDBY)))
+        return;
     const int wave = (int)(threadIdx.x >> 6);
     const int lane = (int)(threadIdx.x & 63);
     LonePair &pr = s_pair[0];
@@ -1793,12 +1804,16 @@ __global__ __launch_bounds__(128) void lone_kernel(Params P, Ctl C) {
         return;
     }
     unsigned gen = 0;
-    if (C.lk_on && lane == 0) atomicAdd(C.lk_active, 1ull);
-    lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen, C.lk_on ? 2 : 0);
-    if (C.lk_on) {
-        if (lane == 0) __hip_atomic_fetch_add(C.lk_active, ~0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        lone_children(P, C, lane, pr, gen);
+    if (!extra) {
+        if (C.lk_on && lane == 0) atomicAdd(C.lk_active, 1ull);
+        lone_interact(P, C, C.lone[blockIdx.x], lane, pr, gen, C.lk_on ? 2 : 0);
+        if (C.lk_on && lane == 0) {
+            /* its children are queued before it counts as finished (release) */
+            __hip_atomic_fetch_add(C.lk_orig, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(C.lk_active, ~0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
+    if (C.lk_on) lone_children(P, C, lane, pr, gen, n_handed);
     if (lane == 0) __hip_atomic_store(&pr.ctl.req, LONE_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -2820,11 +2835,12 @@ struct grm_engine {
     static constexpr unsigned long long EARLY_CAP = 1024;
     LoneRec *d_early = nullptr;
     unsigned long long *d_early_ready = nullptr;
-    /* the lone kernel's children queue (Ctl::lk_*): LK_CAP slots, their ready tags, and the four words
-     * tail, taken, active, standby (one per SMALL_STRIDE), cleared before every lone launch */
+    /* the lone kernel's children queue (Ctl::lk_*): LK_CAP slots, their ready tags, and the five words
+     * tail, taken, active, standby, originals finished (one per SMALL_STRIDE), cleared before every
+     * lone launch */
     static constexpr unsigned long long LK_CAP = 4096;
     LoneRec *d_lk = nullptr;
-    unsigned long long *d_lk_ready = nullptr, *d_lk_words = nullptr;
+    unsigned long long *d_lk_ready = nullptr, *d_lk_words = nullptr; /* words: 5 x SMALL_STRIDE */
     unsigned long long launch_seq = 0;
     size_t waves_rows = 0; /* rows of d_waves the last recorded launch wrote */
     hipStream_t stream2 = nullptr;
@@ -3177,8 +3193,9 @@ int run_passes(grm_engine *e, const grm_init_photon *d_batch, size_t n, int sh, 
             C.lk_taken = e->d_lk_words + 1 * SMALL_STRIDE;
             C.lk_active = e->d_lk_words + 2 * SMALL_STRIDE;
             C.lk_standby = e->d_lk_words + 3 * SMALL_STRIDE;
+            C.lk_orig = e->d_lk_words + 4 * SMALL_STRIDE;
             if (C.lk_on)
-                HIPCHK(e, hipMemsetAsync(e->d_lk_words, 0, 4 * SMALL_STRIDE * sizeof(unsigned long long), e->stream));
+                HIPCHK(e, hipMemsetAsync(e->d_lk_words, 0, 5 * SMALL_STRIDE * sizeof(unsigned long long), e->stream));
             HIPCHK(e, hipEventRecord(e->ev2, e->stream));
             HIPCHK(e, grm_lone_launch(0, (unsigned)e->lone_cap, e->stream, &e->P, sizeof(Params), &C, sizeof(Ctl)));
             HIPCHK(e, hipEventRecord(e->ev3, e->stream));
@@ -3353,7 +3370,7 @@ int grm_engine_create(const grm_header *h, const double *const fields[8], const 
         !hip_ok(e, hipMalloc(&e->d_lk, grm_engine::LK_CAP * sizeof(LoneRec)), "lone children queue") ||
         !hip_ok(e, hipMalloc(&e->d_lk_ready, grm_engine::LK_CAP * sizeof(unsigned long long)), "lone children queue") ||
         !hip_ok(e, hipMemset(e->d_lk_ready, 0, grm_engine::LK_CAP * sizeof(unsigned long long)), "lone children queue") ||
-        !hip_ok(e, hipMalloc(&e->d_lk_words, 4 * SMALL_STRIDE * sizeof(unsigned long long)), "lone children queue"))
+        !hip_ok(e, hipMalloc(&e->d_lk_words, 5 * SMALL_STRIDE * sizeof(unsigned long long)), "lone children queue"))
         return fail();
     if (!hip_ok(e, hipHostMalloc(reinterpret_cast<void **>(&e->pin), sizeof(grm_engine::Pinned),
                                  hipHostMallocMapped | hipHostMallocCoherent),
