@@ -493,10 +493,13 @@ def main():
                        "emit_ms_per_pass": emit_ms / args.steps,
                        "longest_photon_life_steps": max(s["max_photon_steps"] for s in sts),
                        # where each pass's time went beyond its bulk launch: the early worker's launch (beside
-                       # the bulk), the lone-photon kernels after it, the photons they took, the longest life
+                       # the bulk), the lone-photon kernels after it, the photons they took (and the children
+                       # those pairs tracked themselves, GRM_OPT_EARLY_CHILDREN), the longest life
                        "tail_per_pass": [{"bulk_ms": round(s["max_launch_ms"], 1), "early_ms": round(s["early_ms"], 1),
-                                          "n_early": s["n_early"], "lone_ms": round(s["lone_ms"], 1),
-                                          "n_lone": s["n_lone"], "kernels_ms": round(s["last_kernel_ms"], 1),
+                                          "n_early": s["n_early"], "n_early_children": s.get("n_early_children", 0),
+                                          "lone_ms": round(s["lone_ms"], 1), "n_lone": s["n_lone"],
+                                          "n_lone_children": s.get("n_lone_children", 0),
+                                          "kernels_ms": round(s["last_kernel_ms"], 1),
                                           "longest_life": s["max_photon_steps"], "lives_gt_1e5": s["n_long_photons"]}
                                          for s in sts],
                        "tracked_per_pass": sum(s["n_tracked"] for s in sts) // args.steps,
