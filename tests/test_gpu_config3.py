@@ -24,7 +24,7 @@ here every counter is u64):
   - no rank's early-worker queue filled (at 1,500 steps a 1.8e8-photon shard handed over
     888-1,024 photons to a 1,024-slot queue);
   - the JOB's luminosity within LUM_BAR of the photon_n = 1e6 oracle runs' mean
-    (tests/golden/oracle_synth192_pn1e6.json, 12 runs, spread 0.085 %): the estimator is unbiased
+    (tests/golden/oracle_synth192_pn1e6.json, 42 runs, spread 0.11 %): the estimator is unbiased
     whatever the adaptive bias, and at 1.46e9 superphotons its Monte Carlo error is ~0.01 %.
 """
 import json

@@ -127,8 +127,8 @@ N_DEV6 = 8
 
 def test_bench_config_vs_oracle(dump_dir):
     """The bench's own configuration (BASELINE configs[1]): photon_n = 1e6 on the 192^2 dump, tables
-    built on the GPU, as bench.py runs it, against twelve oracle run_simulation runs at photon_n = 1e6
-    (tests/golden/oracle_synth192_pn1e6.*, ~1 h of CPU each): the binned KS test of one traced pass
+    built on the GPU, as bench.py runs it, against 42 oracle run_simulation runs at photon_n = 1e6
+    (tests/golden/oracle_synth192_pn1e6.*, ~1 h of CPU each; seeds 123-164): the binned KS test of one traced pass
     and the counter means of N_DEV6 passes (Welch, |diff| <= Z_MAX standard errors)."""
     import grmonty_amd as GA
     from grmonty_amd.synth_dump import ensure_dump
